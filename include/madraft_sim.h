@@ -1,0 +1,202 @@
+/*
+ * madraft_sim.h — C ABI of the MI355X batched deterministic Raft simulator.
+ *
+ * This is the drop-in boundary for the reference's hot path: the single-seed
+ * MadSim executor + simulated network + Raft node + persister + tester that
+ * `MADSIM_TEST_NUM=N cargo test <name>` runs once per seed
+ * (/root/reference/README.md:44-66). One `mr_batch` runs `n_clusters`
+ * independent seeds of one reference test in lockstep on one GPU.
+ *
+ * Interfaces replaced (reference file:line):
+ *   - `#[madsim::test]` seed loop + MADSIM_TEST_SEED/NUM  (README.md:44-66)
+ *       -> mr_batch_create / mr_batch_run / mr_batch_verdicts
+ *   - RaftTester::new/one/wait/check_* / end                (src/raft/tester.rs:34-358)
+ *       -> scenario programs executed inside mr_batch_run
+ *   - RaftHandle::{new,start,term,is_leader,snapshot,cond_install_snapshot}
+ *                                                            (src/raft/raft.rs:107-168)
+ *       -> device Raft node state machine inside mr_batch_run
+ *   - madsim net stat().msg_count, fs get_file_size          (src/raft/tester.rs:147-158)
+ *       -> mr_counters, persisted-size model
+ *   - panic!(...) + "MADSIM_TEST_SEED=" report               (README.md:44-48)
+ *       -> per-cluster fail code (MR_FAIL_*) + fail time; mr_fail_message()
+ *
+ * Conventions: plain C types, caller-owned buffers, int status (0 = ok,
+ * <0 = error, message in mr_last_error()). One mr_batch per device; a batch is
+ * not thread-safe. The exact simulation semantics are in docs/SEMANTICS.md.
+ */
+#ifndef MADRAFT_SIM_H
+#define MADRAFT_SIM_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MR_ABI_VERSION 1u
+#define MR_MAX_NODES 8u
+#define MR_MAX_MSG_SLOTS 64u
+#define MR_MAX_AE 32u
+
+/* ---- scenarios: one id per reference #[madsim::test] (src/raft/tests.rs) ---- */
+enum mr_scenario {
+  MR_SCN_NONE = 0,
+  MR_SCN_INITIAL_ELECTION_2A = 1,        /* tests.rs:20-46   */
+  MR_SCN_REELECTION_2A = 2,              /* tests.rs:48-78   */
+  MR_SCN_MANY_ELECTION_2A = 3,           /* tests.rs:80-112  */
+  MR_SCN_BASIC_AGREE_2B = 4,             /* tests.rs:114-130 */
+  MR_SCN_FAIL_AGREE_2B = 5,              /* tests.rs:132-161 */
+  MR_SCN_FAIL_NO_AGREE_2B = 6,           /* tests.rs:163-209 */
+  MR_SCN_CONCURRENT_STARTS_2B = 7,       /* tests.rs:211-275 */
+  MR_SCN_REJOIN_2B = 8,                  /* tests.rs:277-313 */
+  MR_SCN_BACKUP_2B = 9,                  /* tests.rs:315-386 */
+  MR_SCN_COUNT_2B = 10,                  /* tests.rs:388-479 */
+  MR_SCN_PERSIST1_2C = 11,               /* tests.rs:481-526 */
+  MR_SCN_PERSIST2_2C = 12,               /* tests.rs:528-572 */
+  MR_SCN_PERSIST3_2C = 13,               /* tests.rs:574-602 */
+  MR_SCN_FIGURE_8_2C = 14,               /* tests.rs:612-660 */
+  MR_SCN_UNRELIABLE_AGREE_2C = 15,       /* tests.rs:662-686 */
+  MR_SCN_FIGURE_8_UNRELIABLE_2C = 16,    /* tests.rs:688-741 */
+  MR_SCN_RELIABLE_CHURN_2C = 17,         /* tests.rs:743-747 */
+  MR_SCN_UNRELIABLE_CHURN_2C = 18,       /* tests.rs:749-753 */
+  MR_SCN_SNAPSHOT_BASIC_2D = 19,         /* tests.rs:913-917 */
+  MR_SCN_SNAPSHOT_INSTALL_2D = 20,       /* tests.rs:919-923 */
+  MR_SCN_SNAPSHOT_INSTALL_UNRELIABLE_2D = 21,       /* tests.rs:925-929 */
+  MR_SCN_SNAPSHOT_INSTALL_CRASH_2D = 22,            /* tests.rs:931-935 */
+  MR_SCN_SNAPSHOT_INSTALL_UNRELIABLE_CRASH_2D = 23, /* tests.rs:937-941 */
+  /* BASELINE.json config 3 read literally: figure_8_unreliable_2c's loop with
+   * crash1/start1 (figure_8_2c, tests.rs:638-649) in place of disconnect. */
+  MR_SCN_FIGURE_8_UNRELIABLE_CRASH = 24,
+  MR_SCN_COUNT_
+};
+
+/* ---- flags ---- */
+#define MR_F_UNRELIABLE 0x1u /* set_unreliable(true) right after RaftTester::new (C2) */
+#define MR_F_NULL_RAFT 0x2u  /* skeleton node: never campaigns (as-shipped raft.rs) */
+#define MR_F_TRACE 0x4u      /* capture per-event trace for the first trace_clusters */
+
+/* ---- verdicts: one code per tester panic site ---- */
+enum mr_fail {
+  MR_PASS = 0,
+  MR_FAIL_ONE_LEADER_NONE = 1,    /* tester.rs:91  "expected one leader, got none" */
+  MR_FAIL_MULTI_LEADER_TERM = 2,  /* tester.rs:83  "term {} has {:?} (>1) leaders" */
+  MR_FAIL_TERM_DISAGREE = 3,      /* tester.rs:105 "servers disagree on term" */
+  MR_FAIL_UNEXPECTED_LEADER = 4,  /* tester.rs:119 "expected no leader, but {} claims..." */
+  MR_FAIL_WAIT_TOO_FEW = 5,       /* tester.rs:198 "only {} decided for index {}; wanted {}" */
+  MR_FAIL_ONE_NO_AGREEMENT = 6,   /* tester.rs:255,261 "one({:?}) failed to reach agreement" */
+  MR_FAIL_TIMEOUT_120S = 7,       /* tester.rs:356 "test took longer than 120 seconds" */
+  MR_FAIL_APPLY_MISMATCH = 8,     /* tester.rs:384-388 "commit index=.. server=.. != .." */
+  MR_FAIL_APPLY_OUT_OF_ORDER = 9, /* tester.rs:393 "server {} apply out of order {}" */
+  MR_FAIL_COMMIT_MISMATCH = 10,   /* tester.rs:411-415 "committed values do not match" */
+  MR_FAIL_UNWRAP_NONE = 11,       /* tester.rs:76,101,118,144,166 unwrap() on a crashed raft */
+  MR_FAIL_LOG_SIZE = 12,          /* tests.rs:894 "log size too large" */
+  MR_FAIL_BASIC_PRECOMMIT = 13,   /* tests.rs:123 "some have committed before start()" */
+  MR_FAIL_BASIC_INDEX = 14,       /* tests.rs:126 "got index {} but expected {}" */
+  MR_FAIL_LEADER_REJECTED = 15,   /* tests.rs:180,202 "leader rejected start" (expect) */
+  MR_FAIL_EXPECTED_INDEX2 = 16,   /* tests.rs:183 "expected index 2, got {}" */
+  MR_FAIL_NO_MAJORITY_COMMIT = 17,/* tests.rs:189 "{} committed but no majority" */
+  MR_FAIL_UNEXPECTED_INDEX = 18,  /* tests.rs:204 "unexpected index {}" */
+  MR_FAIL_CMD_MISSING = 19,       /* tests.rs:266 "cmd {} missing in {:?}" */
+  MR_FAIL_TERM_CHANGED = 20,      /* tests.rs:272,468 "term changed too often" */
+  MR_FAIL_RPC_INITIAL = 21,       /* tests.rs:397-401 "too many or few RPCs..." */
+  MR_FAIL_START_FAILED = 22,      /* tests.rs:434 "start failed" */
+  MR_FAIL_WRONG_VALUE = 23,       /* tests.rs:445-452 "wrong value {:?} committed..." */
+  MR_FAIL_RPC_TOO_MANY = 24,      /* tests.rs:462 "too many RPCs ({}) for {} entries" */
+  MR_FAIL_RPC_IDLE = 25,          /* tests.rs:472-476 "too many RPCs for 1 second of idleness" */
+  MR_FAIL_CHURN_VALUE = 26,       /* tests.rs:852 "didn't find a value" */
+  /* simulator limits (not reference panics): a cluster that hits one is reported, never passed */
+  MR_FAIL_SIM_CAPACITY = 60,      /* a log / apply / sequence capacity of the config was exceeded */
+  MR_FAIL_SIM_EVENT_LIMIT = 61,   /* cfg.max_events processed without a verdict */
+  MR_FAIL_SIM_BAD_PROGRAM = 62,   /* scenario program error (interpreter budget, bad op) */
+  MR_RUNNING = 0xFFFF             /* verdict not reached yet */
+};
+
+typedef struct mr_cfg {
+  uint32_t abi_version;   /* = MR_ABI_VERSION */
+  uint32_t scenario;      /* enum mr_scenario */
+  uint32_t n_nodes;       /* servers, 3..8 (reference default per test if 0) */
+  uint32_t flags;         /* MR_F_* */
+  uint64_t seed_base;     /* cluster c runs seed  seed_base + cluster_base + c */
+  uint64_t cluster_base;  /* global id of this batch's first cluster (multi-GPU shard) */
+  uint64_t n_clusters;    /* clusters in this batch */
+  uint32_t iters;         /* scenario loop count override (0 = the reference's) */
+  uint32_t log_cap;       /* Raft log ring capacity per node, power of two */
+  uint32_t apply_cap;     /* apply-checker index capacity per cluster */
+  uint32_t msg_slots;     /* max in-flight messages per cluster (<= 64) */
+  uint32_t ae_max;        /* max entries per AppendEntries (<= 32) */
+  uint32_t hb_us;         /* leader heartbeat period */
+  uint32_t elect_lo_us;   /* election timeout U[lo, hi) (raft.rs:262: 150..300 ms) */
+  uint32_t elect_hi_us;
+  uint32_t max_events;    /* per-cluster event cap -> MR_FAIL_SIM_EVENT_LIMIT */
+  uint32_t trace_clusters;/* with MR_F_TRACE: the first K clusters keep a trace */
+  uint32_t trace_cap;     /* trace records per traced cluster */
+  int32_t device;         /* HIP device ordinal */
+  uint32_t reserved[6];
+} mr_cfg;
+
+/* Whole-batch counters (sums over clusters unless named max/first). */
+typedef struct mr_counters {
+  uint64_t clusters, done, passed, failed;
+  uint64_t events, ev_msg, ev_timer, ev_tester;
+  uint64_t msgs_sent;      /* every send: madsim stat().msg_count (tester.rs:147-149) */
+  uint64_t drop_clog;      /* endpoint disconnected at send */
+  uint64_t drop_loss;      /* Bernoulli(packet_loss_rate) */
+  uint64_t drop_overflow;  /* more than msg_slots in flight */
+  uint64_t drop_deliver;   /* endpoint disconnected / crashed at delivery */
+  uint64_t drop_stale;     /* RPC reply to a killed incarnation */
+  uint64_t elections, leaders_elected, applies, snapshots, installs;
+  uint64_t entries_shipped;/* log entries carried by AppendEntries */
+  uint64_t virt_time_us;   /* sum of per-cluster virtual end time */
+  uint64_t max_inflight, max_log, max_index;
+  uint64_t first_fail_cluster; /* global cluster id (UINT64_MAX if none) */
+  uint64_t first_fail_code;
+  uint64_t fail_hist[64];  /* verdict histogram by code (index 63 = >= 63) */
+} mr_counters;
+
+typedef struct mr_run_stats {
+  uint64_t launches;       /* step-kernel launches */
+  double kernel_ms;        /* summed step-kernel time (HIP events, batch stream) */
+  double wall_ms;          /* host wall time of mr_batch_run */
+  uint64_t events;         /* events processed in this call */
+  uint64_t remaining;      /* clusters without verdict after the call */
+} mr_run_stats;
+
+/* One trace record per processed event (32 B); docs/SEMANTICS.md §Trace. */
+typedef struct mr_event {
+  uint32_t time_us;
+  uint8_t cls;     /* 0 message, 1 node timer, 2 tester, 3 verdict */
+  uint8_t kind;    /* message type / drop reason / fail code */
+  uint8_t node;    /* destination or timer node (0xFF for tester) */
+  uint8_t role;    /* node role after the event (0 F, 1 C, 2 L, 3 down) */
+  uint32_t aux;    /* message seq / msgs_sent for tester events */
+  uint32_t term, commit, applied, last, snap;
+} mr_event;
+
+typedef struct mr_batch mr_batch;
+
+const char* mr_last_error(void);
+const char* mr_fail_message(uint32_t code);
+const char* mr_scenario_name(uint32_t scenario);
+/* Name as in tests.rs (e.g. "figure_8_unreliable_2c") -> id; 0 if unknown. */
+uint32_t mr_scenario_from_name(const char* name);
+/* Fill cfg with the reference's defaults for `scenario`. */
+int mr_cfg_init(mr_cfg* cfg, uint32_t scenario);
+
+int mr_batch_create(const mr_cfg* cfg, mr_batch** out);
+/* Re-seed and reset every cluster to RaftTester::new state (device-side). */
+int mr_batch_reset(mr_batch* b, uint64_t seed_base);
+/* Run until every cluster has a verdict or max_events_per_call events per
+ * cluster were processed in this call (0 = no per-call bound). */
+int mr_batch_run(mr_batch* b, uint64_t max_events_per_call, mr_run_stats* st);
+/* Per-cluster verdict code, fail/end time (virtual us) and trace digest. */
+int mr_batch_verdicts(mr_batch* b, uint16_t* code, uint32_t* time_us, uint64_t* digest);
+int mr_batch_counters(mr_batch* b, mr_counters* out);
+/* Trace of traced cluster `k` (k < trace_clusters). *n = records written. */
+int mr_trace_get(mr_batch* b, uint32_t k, mr_event* out, size_t cap, size_t* n);
+void mr_batch_destroy(mr_batch* b);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MADRAFT_SIM_H */

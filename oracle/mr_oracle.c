@@ -1,0 +1,1211 @@
+/*
+ * mr_oracle.c — CPU oracle (TEST INFRASTRUCTURE ONLY; see mr_oracle.h).
+ *
+ * One cluster at a time, madsim-shaped: a binary heap of (time, class, tie)
+ * keys holds in-flight messages and node timers (timers are lazily
+ * invalidated by a generation number, as an executor's cancelled timers
+ * would be); the tester script is ordinary sequential C whose sleep() drains
+ * the heap up to its wake time, and whose panics longjmp to the seed loop.
+ * Semantics: docs/SEMANTICS.md. Reference lines are cited per function.
+ */
+#include "mr_oracle.h"
+
+#include <setjmp.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+/* ------------------------------------------------------------------ */
+/* Philox4x32-10 (Salmon, Moraes, Dror, Shaw SC'11; Random123 constants) */
+/* ------------------------------------------------------------------ */
+void mro_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]) {
+  uint32_t c0 = ctr[0], c1 = ctr[1], c2 = ctr[2], c3 = ctr[3];
+  uint32_t k0 = key[0], k1 = key[1];
+  for (int r = 0; r < 10; r++) {
+    if (r) {
+      k0 += 0x9E3779B9u;
+      k1 += 0xBB67AE85u;
+    }
+    uint64_t p0 = (uint64_t)0xD2511F53u * c0;
+    uint64_t p1 = (uint64_t)0xCD9E8D57u * c2;
+    uint32_t n0 = (uint32_t)(p1 >> 32) ^ c1 ^ k0;
+    uint32_t n1 = (uint32_t)p1;
+    uint32_t n2 = (uint32_t)(p0 >> 32) ^ c3 ^ k1;
+    uint32_t n3 = (uint32_t)p0;
+    c0 = n0; c1 = n1; c2 = n2; c3 = n3;
+  }
+  out[0] = c0; out[1] = c1; out[2] = c2; out[3] = c3;
+}
+
+enum { ST_TESTER = 1, ST_ELECT = 2, ST_NET = 3 };
+enum { R_F = 0, R_C = 1, R_L = 2, R_DOWN = 3 };
+enum { M_RV_REQ = 1, M_RV_REP, M_AE_REQ, M_AE_REP, M_IS_REQ, M_IS_REP };
+#define INF_T 0xFFFFFFFFu
+#define LOSS_Q32 429496729u /* floor(0.1 * 2^32), tester.rs:130 */
+
+static inline uint32_t u_range(uint32_t w, uint32_t lo, uint32_t hi) {
+  return lo + (uint32_t)(((uint64_t)w * (uint64_t)(hi - lo)) >> 32);
+}
+
+/* ------------------------------------------------------------------ */
+/* cluster state                                                        */
+/* ------------------------------------------------------------------ */
+typedef struct {
+  uint32_t time, seq;
+  uint8_t type, src, dst, inc;
+  uint32_t term, a, b, c, k;
+  uint64_t v;
+  uint32_t et[MR_MAX_AE];
+  uint64_t ev[MR_MAX_AE];
+} OMsg;
+
+typedef struct {
+  uint32_t term; int32_t voted; uint32_t role; int alive, conn; uint32_t inc;
+  uint32_t commit, applied, last, snap_idx, snap_term; uint64_t snap_val;
+  uint32_t timer_gen, votes;
+  uint32_t next[MR_MAX_NODES], match[MR_MAX_NODES];
+  uint32_t e_ctr, n_ctr;
+  uint32_t* lterm; uint64_t* lval; /* ring of log_cap */
+} ONode;
+
+typedef struct { uint64_t key; uint32_t ref; uint32_t gen; } HEnt;
+
+typedef struct {
+  mr_cfg cfg;
+  uint32_t n, key[2], now, scenario, snapshot_mode, null_raft;
+  uint32_t lat_lo, lat_hi, loss;
+  ONode nd[MR_MAX_NODES];
+  /* network */
+  OMsg pool[MR_MAX_MSG_SLOTS]; uint32_t free_stack[MR_MAX_MSG_SLOTS]; uint32_t n_free;
+  uint32_t inflight;
+  HEnt* heap; uint32_t heap_n, heap_cap;
+  /* tester */
+  uint32_t t_ctr;
+  uint8_t* mask; uint64_t* sval; uint32_t slen[MR_MAX_NODES];
+  /* results */
+  mro_result r;
+  mr_event* trace; size_t trace_cap, n_trace;
+  jmp_buf jb;
+} OSim;
+
+/* ------------------------------------------------------------------ */
+/* trace / verdict                                                      */
+/* ------------------------------------------------------------------ */
+static void rec_push(OSim* s, const mr_event* e) {
+  const uint32_t* w = (const uint32_t*)e;
+  uint64_t h = s->r.digest;
+  for (int i = 0; i < 8; i++) { h ^= w[i]; h *= 0x100000001B3ull; }
+  s->r.digest = h;
+  if (s->trace && s->n_trace < s->trace_cap) s->trace[s->n_trace] = *e;
+  s->n_trace++;
+}
+
+static void rec_node(OSim* s, uint32_t cls, uint32_t kind, uint32_t node, uint32_t aux) {
+  const ONode* d = &s->nd[node];
+  mr_event e;
+  e.time_us = s->now; e.cls = (uint8_t)cls; e.kind = (uint8_t)kind; e.node = (uint8_t)node;
+  e.role = (uint8_t)(d->alive ? d->role : R_DOWN);
+  e.aux = aux; e.term = d->term; e.commit = d->commit; e.applied = d->applied;
+  e.last = d->last; e.snap = d->snap_idx;
+  rec_push(s, &e);
+}
+
+static void rec_simple(OSim* s, uint32_t cls, uint32_t kind) {
+  mr_event e;
+  memset(&e, 0, sizeof e);
+  e.time_us = s->now; e.cls = (uint8_t)cls; e.kind = (uint8_t)kind; e.node = 0xFF;
+  e.aux = (uint32_t)s->r.msgs_sent;
+  rec_push(s, &e);
+}
+
+/* panic!(..): the verdict record, then unwind to the seed loop (README.md:44-48) */
+static void t_fail(OSim* s, uint32_t code) {
+  s->r.code = code; s->r.time_us = s->now;
+  rec_simple(s, 3, code);
+  longjmp(s->jb, 1);
+}
+
+static void count_event(OSim* s) {
+  s->r.events++;
+  if (s->r.events > s->cfg.max_events) t_fail(s, MR_FAIL_SIM_EVENT_LIMIT);
+}
+
+/* ------------------------------------------------------------------ */
+/* executor: binary heap                                                */
+/* ------------------------------------------------------------------ */
+static void heap_push(OSim* s, uint64_t key, uint32_t ref, uint32_t gen) {
+  if (s->heap_n == s->heap_cap) {
+    s->heap_cap = s->heap_cap ? 2 * s->heap_cap : 256;
+    s->heap = (HEnt*)realloc(s->heap, s->heap_cap * sizeof(HEnt));
+  }
+  uint32_t i = s->heap_n++;
+  while (i) {
+    uint32_t p = (i - 1) >> 1;
+    if (s->heap[p].key <= key) break;
+    s->heap[i] = s->heap[p];
+    i = p;
+  }
+  s->heap[i].key = key; s->heap[i].ref = ref; s->heap[i].gen = gen;
+}
+
+static HEnt heap_pop(OSim* s) {
+  HEnt top = s->heap[0];
+  HEnt last = s->heap[--s->heap_n];
+  uint32_t i = 0, n = s->heap_n;
+  for (;;) {
+    uint32_t l = 2 * i + 1;
+    if (l >= n) break;
+    uint32_t m = (l + 1 < n && s->heap[l + 1].key < s->heap[l].key) ? l + 1 : l;
+    if (s->heap[m].key >= last.key) break;
+    s->heap[i] = s->heap[m];
+    i = m;
+  }
+  if (n) s->heap[i] = last;
+  return top;
+}
+
+static void set_timer(OSim* s, uint32_t d, uint32_t t) {
+  ONode* x = &s->nd[d];
+  x->timer_gen++;
+  heap_push(s, ((uint64_t)t << 32) | (1ull << 30) | d, d, x->timer_gen);
+}
+
+/* raft.rs:260-263 generate_election_timeout: U[150,300) ms */
+static void reset_timer(OSim* s, uint32_t d) {
+  ONode* x = &s->nd[d];
+  uint32_t ctr[4] = {x->e_ctr++, d, ST_ELECT, 0}, w[4];
+  mro_philox4x32_10(ctr, s->key, w);
+  set_timer(s, d, s->now + u_range(w[0], s->cfg.elect_lo_us, s->cfg.elect_hi_us));
+}
+
+/* ------------------------------------------------------------------ */
+/* network (madsim net: tester.rs:127-137 config, :147-149 stat)        */
+/* ------------------------------------------------------------------ */
+static void net_send(OSim* s, uint32_t src, uint32_t dst, OMsg* m) {
+  uint32_t seq = (uint32_t)s->r.msgs_sent;
+  s->r.msgs_sent++;
+  ONode* x = &s->nd[src];
+  uint32_t ctr[4] = {x->n_ctr++, src, ST_NET, 0}, w[4];
+  mro_philox4x32_10(ctr, s->key, w);
+  if (!s->nd[src].conn || !s->nd[dst].conn) { s->r.drop_clog++; return; }
+  if (w[0] < s->loss) { s->r.drop_loss++; return; }
+  if (s->inflight >= s->cfg.msg_slots) { s->r.drop_overflow++; return; }
+  if (seq >= (1u << 30)) t_fail(s, MR_FAIL_SIM_CAPACITY);
+  m->time = s->now + u_range(w[1], s->lat_lo, s->lat_hi);
+  m->seq = seq; m->src = (uint8_t)src; m->dst = (uint8_t)dst;
+  uint32_t slot = s->free_stack[--s->n_free];
+  s->pool[slot] = *m;
+  s->inflight++;
+  if (s->inflight > s->r.max_inflight) s->r.max_inflight = s->inflight;
+  heap_push(s, ((uint64_t)m->time << 32) | seq, slot, 0);
+}
+
+/* ------------------------------------------------------------------ */
+/* tester storage (tester.rs:366-428)                                   */
+/* ------------------------------------------------------------------ */
+static void push_and_check(OSim* s, uint32_t i, uint32_t idx, uint64_t v) {
+  if (idx >= s->cfg.apply_cap) t_fail(s, MR_FAIL_SIM_CAPACITY);
+  s->r.applies++;
+  if (s->mask[idx] && s->sval[idx] != v) t_fail(s, MR_FAIL_APPLY_MISMATCH); /* :384 */
+  if (idx > s->slen[i]) t_fail(s, MR_FAIL_APPLY_OUT_OF_ORDER);              /* :393 */
+  if (idx == s->slen[i]) {
+    s->sval[idx] = v;
+    s->mask[idx] |= (uint8_t)(1u << i);
+    s->slen[i]++;
+    if (idx > s->r.max_index) s->r.max_index = idx;
+  }
+}
+
+static void storage_snapshot(OSim* s, uint32_t i, uint32_t idx) { /* :399-402 resize(idx+1) */
+  if (idx >= s->cfg.apply_cap) t_fail(s, MR_FAIL_SIM_CAPACITY);
+  uint32_t nl = idx + 1;
+  for (uint32_t j = nl; j < s->slen[i]; j++) s->mask[j] &= (uint8_t)~(1u << i);
+  s->slen[i] = nl;
+}
+
+static void n_committed(OSim* s, uint32_t idx, uint32_t* cnt, uint64_t* v) { /* :405-422 */
+  if (idx >= s->cfg.apply_cap) { *cnt = 0; *v = 0; return; }
+  *cnt = (uint32_t)__builtin_popcount(s->mask[idx]);
+  *v = s->sval[idx];
+}
+
+/* ------------------------------------------------------------------ */
+/* Raft node (SEMANTICS.md §5; API raft.rs:107-168)                     */
+/* ------------------------------------------------------------------ */
+static inline uint32_t lpos(OSim* s, uint32_t i) { return i & (s->cfg.log_cap - 1); }
+
+static uint32_t term_at(OSim* s, ONode* d, uint32_t i) {
+  if (i == 0) return 0;
+  if (i == d->snap_idx) return d->snap_term;
+  return d->lterm[lpos(s, i)];
+}
+
+static void log_put(OSim* s, ONode* d, uint32_t i, uint32_t t, uint64_t v) {
+  if (i - d->snap_idx > s->cfg.log_cap) t_fail(s, MR_FAIL_SIM_CAPACITY);
+  d->lterm[lpos(s, i)] = t;
+  d->lval[lpos(s, i)] = v;
+  d->last = i;
+  if (i - d->snap_idx > s->r.max_log) s->r.max_log = i - d->snap_idx;
+}
+
+/* tester.rs:303-325 applier: push_and_check, snapshot every SNAPSHOT_INTERVAL */
+static void node_apply(OSim* s, uint32_t me) {
+  ONode* d = &s->nd[me];
+  while (d->applied < d->commit) {
+    uint32_t i = ++d->applied;
+    uint64_t v = d->lval[lpos(s, i)];
+    push_and_check(s, me, i, v);
+    if (s->snapshot_mode && (i + 1) % 10 == 0 && i > d->snap_idx) {
+      d->snap_term = term_at(s, d, i);
+      d->snap_val = v;
+      d->snap_idx = i;
+      s->r.snapshots++;
+    }
+  }
+}
+
+static void send_append(OSim* s, uint32_t me, uint32_t p) {
+  ONode* d = &s->nd[me];
+  OMsg m;
+  m.term = d->term; m.inc = (uint8_t)d->inc;
+  if (d->next[p] <= d->snap_idx) {
+    m.type = M_IS_REQ; m.a = d->snap_idx; m.b = d->snap_term; m.v = d->snap_val;
+    m.c = 0; m.k = 0;
+  } else {
+    uint32_t prev = d->next[p] - 1;
+    uint32_t k = d->last - prev;
+    if (k > s->cfg.ae_max) k = s->cfg.ae_max;
+    m.type = M_AE_REQ; m.a = prev; m.b = term_at(s, d, prev); m.c = d->commit; m.k = k; m.v = 0;
+    for (uint32_t j = 0; j < k; j++) {
+      m.et[j] = d->lterm[lpos(s, prev + 1 + j)];
+      m.ev[j] = d->lval[lpos(s, prev + 1 + j)];
+    }
+    s->r.entries_shipped += k;
+  }
+  net_send(s, me, p, &m);
+}
+
+static void become_leader(OSim* s, uint32_t me) {
+  ONode* d = &s->nd[me];
+  d->role = R_L;
+  s->r.leaders_elected++;
+  for (uint32_t p = 0; p < s->n; p++) { d->next[p] = d->last + 1; d->match[p] = 0; }
+  d->match[me] = d->last;
+  for (uint32_t p = 0; p < s->n; p++)
+    if (p != me) send_append(s, me, p);
+  set_timer(s, me, s->now + s->cfg.hb_us);
+}
+
+static void advance_commit(OSim* s, uint32_t me) {
+  ONode* d = &s->nd[me];
+  uint32_t mv[MR_MAX_NODES];
+  for (uint32_t p = 0; p < s->n; p++) mv[p] = (p == me) ? d->last : d->match[p];
+  /* insertion sort, descending */
+  for (uint32_t i = 1; i < s->n; i++) {
+    uint32_t x = mv[i], j = i;
+    while (j > 0 && mv[j - 1] < x) { mv[j] = mv[j - 1]; j--; }
+    mv[j] = x;
+  }
+  uint32_t N = mv[s->n / 2];
+  if (N > d->commit && term_at(s, d, N) == d->term) {
+    d->commit = N;
+    node_apply(s, me);
+  }
+}
+
+static void on_ack(OSim* s, uint32_t me, uint32_t p, uint32_t x) {
+  ONode* d = &s->nd[me];
+  if (x > d->match[p]) d->match[p] = x;
+  if (x + 1 > d->next[p]) d->next[p] = x + 1;
+  advance_commit(s, me);
+  if (d->next[p] <= d->last) send_append(s, me, p);
+}
+
+static void reply(OSim* s, uint32_t me, const OMsg* req, uint32_t type, uint32_t a, uint32_t b) {
+  OMsg m;
+  m.type = (uint8_t)type; m.inc = req->inc; m.term = s->nd[me].term;
+  m.a = a; m.b = b; m.c = 0; m.k = 0; m.v = 0;
+  net_send(s, me, req->src, &m);
+}
+
+static void deliver(OSim* s, OMsg* m) {
+  uint32_t me = m->dst;
+  ONode* d = &s->nd[me];
+  if (!d->alive || !d->conn || !s->nd[m->src].conn) {
+    s->r.drop_deliver++;
+    rec_node(s, 0, 16, me, m->seq);
+    return;
+  }
+  int is_reply = (m->type == M_RV_REP || m->type == M_AE_REP || m->type == M_IS_REP);
+  if (is_reply && m->inc != (uint8_t)d->inc) {
+    s->r.drop_stale++;
+    rec_node(s, 0, 17, me, m->seq);
+    return;
+  }
+  if (m->term > d->term) { /* step down */
+    d->term = m->term; d->voted = -1; d->votes = 0;
+    if (d->role == R_L) reset_timer(s, me);
+    d->role = R_F;
+  }
+  switch (m->type) {
+    case M_RV_REQ: {
+      uint32_t lt = term_at(s, d, d->last);
+      int up = (m->c > lt) || (m->c == lt && m->b >= d->last);
+      int granted = (m->term == d->term) && (d->voted < 0 || d->voted == (int32_t)m->a) && up;
+      if (granted) { d->voted = (int32_t)m->a; reset_timer(s, me); }
+      reply(s, me, m, M_RV_REP, (uint32_t)granted, 0);
+    } break;
+    case M_RV_REP:
+      if (d->role == R_C && m->term == d->term && m->a) {
+        d->votes |= 1u << m->src;
+        if ((uint32_t)__builtin_popcount(d->votes) > s->n / 2) become_leader(s, me);
+      }
+      break;
+    case M_AE_REQ: {
+      if (m->term < d->term) { reply(s, me, m, M_AE_REP, 0, 0); break; }
+      if (d->role == R_C) d->role = R_F;
+      reset_timer(s, me);
+      uint32_t prev = m->a, pterm = m->b, j0 = 0;
+      if (prev < d->snap_idx) {
+        uint32_t skip = d->snap_idx - prev;
+        j0 = skip < m->k ? skip : m->k;
+        prev = d->snap_idx; pterm = d->snap_term;
+      }
+      if (prev > d->last) { reply(s, me, m, M_AE_REP, 0, d->last + 1); break; }
+      if (term_at(s, d, prev) != pterm) {
+        uint32_t ct = term_at(s, d, prev), x = prev;
+        while (x - 1 > d->snap_idx && term_at(s, d, x - 1) == ct) x--;
+        reply(s, me, m, M_AE_REP, 0, x);
+        break;
+      }
+      for (uint32_t j = j0; j < m->k; j++) {
+        uint32_t i = m->a + 1 + j;
+        if (i <= d->last && term_at(s, d, i) == m->et[j]) continue;
+        log_put(s, d, i, m->et[j], m->ev[j]); /* truncates to i-1, appends */
+      }
+      uint32_t lc = m->a + m->k;
+      if (m->c < lc) lc = m->c;
+      if (lc > d->commit) { d->commit = lc; node_apply(s, me); }
+      reply(s, me, m, M_AE_REP, 1, m->a + m->k);
+    } break;
+    case M_AE_REP:
+      if (d->role != R_L || m->term != d->term) break;
+      if (m->a) {
+        on_ack(s, me, m->src, m->b);
+      } else {
+        uint32_t x = m->b, lo = d->match[m->src] + 1, hi = d->last + 1;
+        if (x < lo) x = lo;
+        if (x > hi) x = hi;
+        d->next[m->src] = x;
+        send_append(s, me, m->src);
+      }
+      break;
+    case M_IS_REQ: {
+      if (m->term < d->term) { reply(s, me, m, M_IS_REP, 0, 0); break; }
+      if (d->role == R_C) d->role = R_F;
+      reset_timer(s, me);
+      uint32_t idx = m->a;
+      if (idx > d->commit) {
+        if (!(idx <= d->last && term_at(s, d, idx) == m->b)) d->last = idx;
+        d->snap_idx = idx; d->snap_term = m->b; d->snap_val = m->v;
+        d->commit = idx; d->applied = idx;
+        storage_snapshot(s, me, idx);
+        s->r.installs++;
+      }
+      reply(s, me, m, M_IS_REP, 0, idx);
+    } break;
+    case M_IS_REP:
+      if (d->role == R_L && m->term == d->term && m->b > 0) on_ack(s, me, m->src, m->b);
+      break;
+  }
+  rec_node(s, 0, m->type, me, m->seq);
+}
+
+static void on_timer(OSim* s, uint32_t me) {
+  ONode* d = &s->nd[me];
+  if (d->role == R_L) {
+    for (uint32_t p = 0; p < s->n; p++)
+      if (p != me) send_append(s, me, p);
+    set_timer(s, me, s->now + s->cfg.hb_us);
+    rec_node(s, 1, 1, me, 0);
+    return;
+  }
+  d->term++; d->voted = (int32_t)me; d->role = R_C; d->votes = 1u << me;
+  s->r.elections++;
+  reset_timer(s, me);
+  OMsg m;
+  m.type = M_RV_REQ; m.inc = (uint8_t)d->inc; m.term = d->term;
+  m.a = me; m.b = d->last; m.c = term_at(s, d, d->last); m.k = 0; m.v = 0;
+  for (uint32_t p = 0; p < s->n; p++)
+    if (p != me) net_send(s, me, p, &m);
+  rec_node(s, 1, 0, me, 0);
+}
+
+/* drain the executor up to (target, TESTER): every message/timer with time <= target */
+static void run_until(OSim* s, uint32_t target) {
+  while (s->heap_n && (uint32_t)(s->heap[0].key >> 32) <= target) {
+    HEnt e = heap_pop(s);
+    uint32_t cls = (uint32_t)(e.key >> 30) & 3u;
+    if (cls == 1) {
+      ONode* d = &s->nd[e.ref];
+      if (!d->alive || e.gen != d->timer_gen) continue; /* cancelled timer */
+      s->now = (uint32_t)(e.key >> 32);
+      count_event(s);
+      s->r.ev_timer++;
+      on_timer(s, e.ref);
+    } else {
+      OMsg m = s->pool[e.ref];
+      s->free_stack[s->n_free++] = e.ref;
+      s->inflight--;
+      s->now = m.time;
+      count_event(s);
+      s->r.ev_msg++;
+      deliver(s, &m);
+    }
+  }
+  s->now = target;
+}
+
+/* ------------------------------------------------------------------ */
+/* tester API (src/raft/tester.rs)                                      */
+/* ------------------------------------------------------------------ */
+static void t_sleep(OSim* s, uint32_t us) { /* time::sleep */
+  rec_simple(s, 2, 0); /* the tester segment that ends here */
+  uint64_t target = (uint64_t)s->now + us;
+  if (target >= INF_T) t_fail(s, MR_FAIL_SIM_CAPACITY);
+  run_until(s, (uint32_t)target);
+  count_event(s);
+  s->r.ev_tester++;
+}
+
+static void t_draw(OSim* s, uint32_t w[4]) {
+  uint32_t ctr[4] = {s->t_ctr++, 0, ST_TESTER, 0};
+  mro_philox4x32_10(ctr, s->key, w);
+}
+static uint32_t t_range(OSim* s, uint32_t lo, uint32_t hi) {
+  uint32_t w[4]; t_draw(s, w); return u_range(w[0], lo, hi);
+}
+static int t_bool(OSim* s, uint32_t p_q32) { uint32_t w[4]; t_draw(s, w); return w[0] < p_q32; }
+static uint64_t t_entry(OSim* s) { /* tests.rs:943-951 gen_entry */
+  uint32_t w[4]; t_draw(s, w); return ((uint64_t)w[1] << 32) | w[0];
+}
+
+static void t_set_unreliable(OSim* s, int u) { /* tester.rs:127-137 */
+  if (u) { s->loss = LOSS_Q32; s->lat_lo = 1000; s->lat_hi = 27000; }
+  else { s->loss = 0; s->lat_lo = 1000; s->lat_hi = 10000; }
+}
+
+static ONode* t_raft(OSim* s, uint32_t i) { /* rafts[i].as_ref().unwrap() */
+  if (!s->nd[i].alive) t_fail(s, MR_FAIL_UNWRAP_NONE);
+  return &s->nd[i];
+}
+static int t_is_started(OSim* s, uint32_t i) { return s->nd[i].alive; }
+static int t_is_connected(OSim* s, uint32_t i) { return s->nd[i].conn; }
+static uint32_t t_term(OSim* s, uint32_t i) { return t_raft(s, i)->term; }
+static uint32_t t_rpc_total(OSim* s) { return (uint32_t)(s->r.msgs_sent / 2); }
+
+/* tester.rs:165-171 -> raft.rs:238-244 */
+static int t_start(OSim* s, uint32_t i, uint64_t v, uint32_t* idx, uint32_t* term) {
+  ONode* d = t_raft(s, i);
+  if (s->null_raft || d->role != R_L) return 0; /* Err(NotLeader((me+1)%n)) */
+  log_put(s, d, d->last + 1, d->term, v);
+  d->match[i] = d->last;
+  *idx = d->last; *term = d->term;
+  return 1;
+}
+
+static void t_connect(OSim* s, uint32_t i) { s->nd[i].conn = 1; }
+static void t_disconnect(OSim* s, uint32_t i) { s->nd[i].conn = 0; }
+
+static void t_crash1(OSim* s, uint32_t i) { /* tester.rs:329-333 */
+  ONode* d = &s->nd[i];
+  d->alive = 0;
+  d->timer_gen++;
+}
+
+static void t_start1(OSim* s, uint32_t i) { /* tester.rs:293-327 + raft.rs:108-122 restore */
+  t_crash1(s, i);
+  ONode* d = &s->nd[i];
+  d->alive = 1; d->inc++; d->role = R_F; d->votes = 0;
+  d->commit = d->snap_idx; d->applied = d->snap_idx;
+  if (!s->null_raft) reset_timer(s, i);
+}
+
+static uint32_t t_log_size(OSim* s) { /* tester.rs:152-158 + SEMANTICS §5 size model */
+  uint32_t mx = 0;
+  for (uint32_t i = 0; i < s->n; i++) {
+    ONode* d = &s->nd[i];
+    uint32_t sz = 32 + (d->voted >= 0 ? 9 : 1) + 24 * (d->last - d->snap_idx);
+    if (sz > mx) mx = sz;
+  }
+  return mx;
+}
+
+/* tester.rs:64-92 */
+static uint32_t t_check_one_leader(OSim* s) {
+  for (int it = 0; it < 10; it++) {
+    t_sleep(s, t_range(s, 450000, 550000));
+    uint32_t lt[MR_MAX_NODES], ln[MR_MAX_NODES], nl = 0;
+    for (uint32_t i = 0; i < s->n; i++) {
+      if (!s->nd[i].conn) continue;
+      ONode* d = t_raft(s, i);
+      if (!s->null_raft && d->role == R_L) { lt[nl] = d->term; ln[nl] = i; nl++; }
+    }
+    for (uint32_t a = 0; a < nl; a++)
+      for (uint32_t b = a + 1; b < nl; b++)
+        if (lt[a] == lt[b]) t_fail(s, MR_FAIL_MULTI_LEADER_TERM);
+    if (nl) {
+      uint32_t best = 0;
+      for (uint32_t a = 1; a < nl; a++)
+        if (lt[a] > lt[best]) best = a;
+      return ln[best];
+    }
+  }
+  t_fail(s, MR_FAIL_ONE_LEADER_NONE);
+  return 0;
+}
+
+/* tester.rs:95-109 */
+static uint32_t t_check_terms(OSim* s) {
+  uint32_t term = 0;
+  for (uint32_t i = 0; i < s->n; i++) {
+    if (!s->nd[i].conn) continue;
+    uint32_t x = t_term(s, i);
+    if (term == 0) term = x;
+    else if (term != x) t_fail(s, MR_FAIL_TERM_DISAGREE);
+  }
+  return term;
+}
+
+/* tester.rs:112-122 */
+static void t_check_no_leader(OSim* s) {
+  for (uint32_t i = 0; i < s->n; i++) {
+    if (!s->nd[i].conn) continue;
+    ONode* d = t_raft(s, i);
+    if (!s->null_raft && d->role == R_L) t_fail(s, MR_FAIL_UNEXPECTED_LEADER);
+  }
+}
+
+/* tester.rs:175-201; returns 1 and *v on Some */
+static int t_wait(OSim* s, uint32_t index, uint32_t n, int has_st, uint32_t start_term, uint64_t* v) {
+  uint32_t to = 10000, cnt;
+  uint64_t val;
+  for (int it = 0; it < 30; it++) {
+    n_committed(s, index, &cnt, &val);
+    if (cnt >= n) break;
+    t_sleep(s, to);
+    if (to < 1000000) to *= 2;
+    if (has_st)
+      for (uint32_t i = 0; i < s->n; i++)
+        if (s->nd[i].alive && s->nd[i].term > start_term) return 0;
+  }
+  n_committed(s, index, &cnt, &val);
+  if (cnt < n) t_fail(s, MR_FAIL_WAIT_TOO_FEW);
+  *v = val;
+  return cnt > 0;
+}
+
+/* tester.rs:216-262 */
+static uint32_t t_one(OSim* s, uint64_t cmd, uint32_t expected, int retry) {
+  uint32_t t0 = s->now, starts = 0;
+  while (s->now - t0 < 10000000u) {
+    int have = 0;
+    uint32_t index = 0, term;
+    for (uint32_t k = 0; k < s->n; k++) {
+      starts = (starts + 1) % s->n;
+      if (!t_is_connected(s, starts) || !t_is_started(s, starts)) continue;
+      if (t_start(s, starts, cmd, &index, &term)) { have = 1; break; }
+    }
+    if (have) {
+      uint32_t t1 = s->now;
+      while (s->now - t1 < 2000000u) {
+        uint32_t cnt; uint64_t v;
+        n_committed(s, index, &cnt, &v);
+        if (cnt > 0 && cnt >= expected && v == cmd) return index;
+        t_sleep(s, 20000);
+      }
+      if (!retry) t_fail(s, MR_FAIL_ONE_NO_AGREEMENT);
+    } else {
+      t_sleep(s, 50000);
+    }
+  }
+  t_fail(s, MR_FAIL_ONE_NO_AGREEMENT);
+  return 0;
+}
+
+static void t_end(OSim* s) { /* tester.rs:339-358 */
+  if (s->now > 120000000u) t_fail(s, MR_FAIL_TIMEOUT_120S);
+  s->r.code = MR_PASS; s->r.time_us = s->now;
+  rec_simple(s, 3, MR_PASS);
+}
+
+/* RaftTester::new / new_with_snapshot (tester.rs:34-60) */
+static void t_new(OSim* s, int snapshot) {
+  s->snapshot_mode = (uint32_t)snapshot;
+  for (uint32_t i = 0; i < s->n; i++) { t_start1(s, i); t_connect(s, i); }
+  if (s->cfg.flags & MR_F_UNRELIABLE) t_set_unreliable(s, 1);
+}
+
+/* ------------------------------------------------------------------ */
+/* scenarios (src/raft/tests.rs), straight-line                          */
+/* ------------------------------------------------------------------ */
+#define ELECTION_US 1000000u /* RAFT_ELECTION_TIMEOUT tests.rs:18 */
+static uint32_t iters_or(OSim* s, uint32_t d) { return s->cfg.iters ? s->cfg.iters : d; }
+
+static void scn_initial_election(OSim* s) { /* tests.rs:20-46 */
+  t_new(s, 0);
+  t_check_one_leader(s);
+  t_sleep(s, 50000);
+  uint32_t term1 = t_check_terms(s);
+  t_sleep(s, 2 * ELECTION_US);
+  uint32_t term2 = t_check_terms(s);
+  (void)term1; (void)term2; /* warn! only */
+  t_check_one_leader(s);
+  t_end(s);
+}
+
+static void scn_reelection(OSim* s) { /* tests.rs:48-78 */
+  uint32_t n = s->n;
+  t_new(s, 0);
+  uint32_t l1 = t_check_one_leader(s);
+  t_disconnect(s, l1);
+  t_check_one_leader(s);
+  t_connect(s, l1);
+  uint32_t l2 = t_check_one_leader(s);
+  t_disconnect(s, l2);
+  t_disconnect(s, (l2 + 1) % n);
+  t_sleep(s, 2 * ELECTION_US);
+  t_check_no_leader(s);
+  t_connect(s, (l2 + 1) % n);
+  t_check_one_leader(s);
+  t_connect(s, l2);
+  t_check_one_leader(s);
+  t_end(s);
+}
+
+static void scn_many_election(OSim* s) { /* tests.rs:80-112 */
+  uint32_t n = s->n, iters = iters_or(s, 10);
+  t_new(s, 0);
+  t_check_one_leader(s);
+  for (uint32_t it = 0; it < iters; it++) {
+    uint32_t i1 = t_range(s, 0, n), i2 = t_range(s, 0, n), i3 = t_range(s, 0, n);
+    t_disconnect(s, i1); t_disconnect(s, i2); t_disconnect(s, i3);
+    t_check_one_leader(s);
+    t_connect(s, i1); t_connect(s, i2); t_connect(s, i3);
+  }
+  t_check_one_leader(s);
+  t_end(s);
+}
+
+static void scn_basic_agree(OSim* s) { /* tests.rs:114-130 */
+  t_new(s, 0);
+  for (uint32_t index = 1; index <= 3; index++) {
+    uint32_t nd; uint64_t v;
+    n_committed(s, index, &nd, &v);
+    if (nd != 0) t_fail(s, MR_FAIL_BASIC_PRECOMMIT);
+    uint32_t x = t_one(s, (uint64_t)index * 100, s->n, 0);
+    if (x != index) t_fail(s, MR_FAIL_BASIC_INDEX);
+  }
+  t_end(s);
+}
+
+static void scn_fail_agree(OSim* s) { /* tests.rs:132-161 */
+  uint32_t n = s->n;
+  t_new(s, 0);
+  t_one(s, 101, n, 0);
+  uint32_t leader = t_check_one_leader(s);
+  t_disconnect(s, (leader + 1) % n);
+  t_one(s, 102, n - 1, 0);
+  t_one(s, 103, n - 1, 0);
+  t_sleep(s, ELECTION_US);
+  t_one(s, 104, n - 1, 0);
+  t_one(s, 105, n - 1, 0);
+  t_connect(s, (leader + 1) % n);
+  t_one(s, 106, n, 1);
+  t_sleep(s, ELECTION_US);
+  t_one(s, 107, n, 1);
+  t_end(s);
+}
+
+static void scn_fail_no_agree(OSim* s) { /* tests.rs:163-209 */
+  uint32_t n = s->n, idx, term;
+  t_new(s, 0);
+  t_one(s, 10, n, 0);
+  uint32_t leader = t_check_one_leader(s);
+  t_disconnect(s, (leader + 1) % n);
+  t_disconnect(s, (leader + 2) % n);
+  t_disconnect(s, (leader + 3) % n);
+  if (!t_start(s, leader, 20, &idx, &term)) t_fail(s, MR_FAIL_LEADER_REJECTED);
+  if (idx != 2) t_fail(s, MR_FAIL_EXPECTED_INDEX2);
+  t_sleep(s, 2 * ELECTION_US);
+  uint32_t nc; uint64_t v;
+  n_committed(s, idx, &nc, &v);
+  if (nc != 0) t_fail(s, MR_FAIL_NO_MAJORITY_COMMIT);
+  t_connect(s, (leader + 1) % n);
+  t_connect(s, (leader + 2) % n);
+  t_connect(s, (leader + 3) % n);
+  uint32_t leader2 = t_check_one_leader(s);
+  uint32_t idx2;
+  if (!t_start(s, leader2, 30, &idx2, &term)) t_fail(s, MR_FAIL_LEADER_REJECTED);
+  if (idx2 < 2 || idx2 > 3) t_fail(s, MR_FAIL_UNEXPECTED_INDEX);
+  t_one(s, 1000, n, 1);
+  t_end(s);
+}
+
+static void scn_concurrent_starts(OSim* s) { /* tests.rs:211-275 */
+  uint32_t n = s->n;
+  t_new(s, 0);
+  int success = 0;
+  for (int tried = 0; tried < 5; tried++) {
+    if (tried > 0) t_sleep(s, 3000000);
+    uint32_t leader = t_check_one_leader(s), idx, term, st;
+    if (!t_start(s, leader, 1, &idx, &term)) continue;
+    uint32_t idxes[5], ni = 0;
+    for (uint32_t ii = 0; ii < 5; ii++) {
+      uint32_t i2;
+      if (t_start(s, leader, 100 + ii, &i2, &st) && st == term) idxes[ni++] = i2;
+    }
+    int changed = 0;
+    for (uint32_t j = 0; j < n; j++)
+      if (t_term(s, j) != term) { changed = 1; break; }
+    if (changed) continue;
+    uint64_t cmds[5]; uint32_t nc = 0;
+    for (uint32_t q = 0; q < ni; q++) {
+      uint64_t v;
+      if (t_wait(s, idxes[q], n, 1, term, &v)) cmds[nc++] = v;
+    }
+    for (uint32_t ii = 0; ii < 5; ii++) {
+      int ok = 0;
+      for (uint32_t q = 0; q < nc; q++) if (cmds[q] == 100 + ii) ok = 1;
+      if (!ok) t_fail(s, MR_FAIL_CMD_MISSING);
+    }
+    success = 1;
+    break;
+  }
+  if (!success) t_fail(s, MR_FAIL_TERM_CHANGED);
+  t_end(s);
+}
+
+static void scn_rejoin(OSim* s) { /* tests.rs:277-313 */
+  uint32_t n = s->n, idx, term;
+  t_new(s, 0);
+  t_one(s, 101, n, 1);
+  uint32_t l1 = t_check_one_leader(s);
+  t_disconnect(s, l1);
+  t_start(s, l1, 102, &idx, &term);
+  t_start(s, l1, 103, &idx, &term);
+  t_start(s, l1, 104, &idx, &term);
+  t_one(s, 103, 2, 1);
+  uint32_t l2 = t_check_one_leader(s);
+  t_disconnect(s, l2);
+  t_connect(s, l1);
+  t_one(s, 104, 2, 1);
+  t_connect(s, l2);
+  t_one(s, 105, n, 1);
+  t_end(s);
+}
+
+static void scn_backup(OSim* s) { /* tests.rs:315-386 */
+  uint32_t n = s->n, idx, term;
+  t_new(s, 0);
+  t_one(s, t_entry(s), n, 1);
+  uint32_t l1 = t_check_one_leader(s);
+  t_disconnect(s, (l1 + 2) % n); t_disconnect(s, (l1 + 3) % n); t_disconnect(s, (l1 + 4) % n);
+  for (int i = 0; i < 50; i++) { uint64_t e = t_entry(s); t_start(s, l1, e, &idx, &term); }
+  t_sleep(s, ELECTION_US / 2);
+  t_disconnect(s, (l1 + 0) % n); t_disconnect(s, (l1 + 1) % n);
+  t_connect(s, (l1 + 2) % n); t_connect(s, (l1 + 3) % n); t_connect(s, (l1 + 4) % n);
+  for (int i = 0; i < 50; i++) t_one(s, t_entry(s), 3, 1);
+  uint32_t l2 = t_check_one_leader(s);
+  uint32_t other = (l1 + 2) % n;
+  if (l2 == other) other = (l2 + 1) % n;
+  t_disconnect(s, other);
+  for (int i = 0; i < 50; i++) { uint64_t e = t_entry(s); t_start(s, l2, e, &idx, &term); }
+  t_sleep(s, ELECTION_US / 2);
+  for (uint32_t i = 0; i < n; i++) t_disconnect(s, i);
+  t_connect(s, (l1 + 0) % n); t_connect(s, (l1 + 1) % n); t_connect(s, other);
+  for (int i = 0; i < 50; i++) t_one(s, t_entry(s), 3, 1);
+  for (uint32_t i = 0; i < n; i++) t_connect(s, i);
+  t_one(s, t_entry(s), n, 1);
+  t_end(s);
+}
+
+static void scn_count(OSim* s) { /* tests.rs:388-479 */
+  uint32_t n = s->n;
+  t_new(s, 0);
+  t_check_one_leader(s);
+  uint32_t total1 = t_rpc_total(s);
+  if (total1 < 1 || total1 > 30) t_fail(s, MR_FAIL_RPC_INITIAL);
+  uint32_t total2 = 0;
+  int success = 0;
+  for (int tried = 0; tried < 5 && !success; tried++) {
+    if (tried > 0) t_sleep(s, 3000000);
+    uint32_t leader = t_check_one_leader(s);
+    total1 = t_rpc_total(s);
+    const uint32_t iters = 10;
+    uint32_t starti, term, idx, st;
+    if (!t_start(s, leader, 1, &starti, &term)) continue;
+    uint64_t cmds[12];
+    int outer = 0;
+    for (uint32_t i = 1; i < iters + 2; i++) {
+      uint64_t x = t_entry(s); /* random.gen::<u64>() */
+      cmds[i - 1] = x;
+      if (t_start(s, leader, x, &idx, &st)) {
+        if (st != term) { outer = 1; break; }
+        if (starti + i != idx) t_fail(s, MR_FAIL_START_FAILED);
+      } else { outer = 1; break; }
+    }
+    if (outer) continue;
+    for (uint32_t i = 1; i <= iters; i++) {
+      uint64_t v;
+      if (t_wait(s, starti + i, n, 1, term, &v) && v != cmds[i - 1]) t_fail(s, MR_FAIL_WRONG_VALUE);
+    }
+    int changed = 0;
+    for (uint32_t i = 0; i < n; i++)
+      if (t_term(s, i) != term) { changed = 1; break; }
+    if (changed) continue;
+    total2 = t_rpc_total(s);
+    if (total2 - total1 > (iters + 1 + 3) * 3) t_fail(s, MR_FAIL_RPC_TOO_MANY);
+    success = 1;
+  }
+  if (!success) t_fail(s, MR_FAIL_TERM_CHANGED);
+  t_sleep(s, ELECTION_US);
+  uint32_t total3 = t_rpc_total(s);
+  if (total3 - total2 > 3 * 20) t_fail(s, MR_FAIL_RPC_IDLE);
+  t_end(s);
+}
+
+static void scn_persist1(OSim* s) { /* tests.rs:481-526 */
+  uint32_t n = s->n;
+  uint64_t v;
+  t_new(s, 0);
+  t_one(s, 11, n, 1);
+  for (uint32_t i = 0; i < n; i++) t_start1(s, i);
+  for (uint32_t i = 0; i < n; i++) { t_disconnect(s, i); t_connect(s, i); }
+  t_one(s, 12, n, 1);
+  uint32_t l1 = t_check_one_leader(s);
+  t_disconnect(s, l1); t_start1(s, l1); t_connect(s, l1);
+  t_one(s, 13, n, 1);
+  uint32_t l2 = t_check_one_leader(s);
+  t_disconnect(s, l2);
+  t_one(s, 14, n - 1, 1);
+  t_start1(s, l2); t_connect(s, l2);
+  t_wait(s, 4, n, 0, 0, &v);
+  uint32_t i3 = (t_check_one_leader(s) + 1) % n;
+  t_disconnect(s, i3);
+  t_one(s, 15, n - 1, 1);
+  t_start1(s, i3); t_connect(s, i3);
+  t_one(s, 16, n, 1);
+  t_end(s);
+}
+
+static void scn_persist2(OSim* s) { /* tests.rs:528-572 */
+  uint32_t n = s->n;
+  uint64_t index = 1;
+  t_new(s, 0);
+  for (int k = 0; k < 5; k++) {
+    t_one(s, 10 + index, n, 1); index++;
+    uint32_t l1 = t_check_one_leader(s);
+    t_disconnect(s, (l1 + 1) % n); t_disconnect(s, (l1 + 2) % n);
+    t_one(s, 10 + index, n - 2, 1); index++;
+    t_disconnect(s, (l1 + 0) % n); t_disconnect(s, (l1 + 3) % n); t_disconnect(s, (l1 + 4) % n);
+    t_start1(s, (l1 + 1) % n); t_start1(s, (l1 + 2) % n);
+    t_connect(s, (l1 + 1) % n); t_connect(s, (l1 + 2) % n);
+    t_sleep(s, ELECTION_US);
+    t_start1(s, (l1 + 3) % n); t_connect(s, (l1 + 3) % n);
+    t_one(s, 10 + index, n - 2, 1); index++;
+    t_connect(s, (l1 + 4) % n); t_connect(s, (l1 + 0) % n);
+  }
+  t_one(s, 1000, n, 1);
+  t_end(s);
+}
+
+static void scn_persist3(OSim* s) { /* tests.rs:574-602 */
+  uint32_t n = s->n;
+  t_new(s, 0);
+  t_one(s, 101, 3, 1);
+  uint32_t leader = t_check_one_leader(s);
+  t_disconnect(s, (leader + 2) % n);
+  t_one(s, 102, 2, 1);
+  t_crash1(s, (leader + 0) % n); t_crash1(s, (leader + 1) % n);
+  t_connect(s, (leader + 2) % n);
+  t_start1(s, (leader + 0) % n); t_connect(s, (leader + 0) % n);
+  t_one(s, 103, 2, 1);
+  t_start1(s, (leader + 1) % n); t_connect(s, (leader + 1) % n);
+  t_one(s, 104, n, 1);
+  t_end(s);
+}
+
+static uint32_t fig8_delay(OSim* s) { /* tests.rs:631-635 / 711-715 */
+  if (t_bool(s, LOSS_Q32)) return t_range(s, 0, ELECTION_US / 2);
+  return t_range(s, 0, 13000);
+}
+
+static void scn_figure_8(OSim* s) { /* tests.rs:612-660 (+ unreliable variant, config 3) */
+  uint32_t n = s->n, iters = iters_or(s, 1000), idx, term;
+  t_new(s, 0);
+  if (s->scenario == MR_SCN_FIGURE_8_UNRELIABLE_CRASH) t_set_unreliable(s, 1);
+  t_one(s, t_entry(s), 1, 1);
+  uint32_t nup = n;
+  for (uint32_t it = 0; it < iters; it++) {
+    int leader = -1;
+    for (uint32_t i = 0; i < n; i++)
+      if (t_is_started(s, i)) {
+        uint64_t e = t_entry(s);
+        if (t_start(s, i, e, &idx, &term)) leader = (int)i;
+      }
+    t_sleep(s, fig8_delay(s));
+    if (leader >= 0) { t_crash1(s, (uint32_t)leader); nup--; }
+    if (nup < 3) {
+      uint32_t x = t_range(s, 0, n);
+      if (!t_is_started(s, x)) { t_start1(s, x); nup++; }
+    }
+  }
+  for (uint32_t i = 0; i < n; i++)
+    if (!t_is_started(s, i)) t_start1(s, i);
+  t_one(s, t_entry(s), n, 1);
+  t_end(s);
+}
+
+static void scn_figure_8_unreliable(OSim* s) { /* tests.rs:688-741 */
+  uint32_t n = s->n, iters = iters_or(s, 1000), idx, term;
+  t_new(s, 0);
+  t_set_unreliable(s, 1);
+  t_one(s, t_entry(s), 1, 1);
+  uint32_t nup = n;
+  for (uint32_t it = 0; it < iters; it++) {
+    int leader = -1;
+    for (uint32_t i = 0; i < n; i++) {
+      uint64_t e = t_entry(s);
+      if (t_start(s, i, e, &idx, &term) && t_is_connected(s, i)) leader = (int)i;
+    }
+    t_sleep(s, fig8_delay(s));
+    if (leader >= 0 && t_range(s, 0, 1000) < 500) { t_disconnect(s, (uint32_t)leader); nup--; }
+    if (nup < 3) {
+      uint32_t x = t_range(s, 0, n);
+      if (!t_is_connected(s, x)) { t_connect(s, x); nup++; }
+    }
+  }
+  for (uint32_t i = 0; i < n; i++) t_connect(s, i);
+  t_one(s, t_entry(s), n, 1);
+  t_end(s);
+}
+
+static void scn_snap_common(OSim* s, int disconnect, int reliable, int crash) { /* tests.rs:858-911 */
+  const uint32_t MAX_LOG_SIZE = 2000;
+  uint32_t n = s->n, iters = iters_or(s, 30), idx, term;
+  t_new(s, 1);
+  t_set_unreliable(s, !reliable);
+  t_one(s, t_entry(s), n, 1);
+  uint32_t leader1 = t_check_one_leader(s);
+  for (uint32_t i = 0; i < iters; i++) {
+    uint32_t victim = (leader1 + 1) % n, sender = leader1;
+    if (i % 3 == 1) { sender = (leader1 + 1) % n; victim = leader1; }
+    if (disconnect) { t_disconnect(s, victim); t_one(s, t_entry(s), n - 1, 1); }
+    if (crash) { t_crash1(s, victim); t_one(s, t_entry(s), n - 1, 1); }
+    for (int k = 0; k <= 10; k++) { uint64_t e = t_entry(s); t_start(s, sender, e, &idx, &term); }
+    t_one(s, t_entry(s), n - 1, 1);
+    if (t_log_size(s) >= MAX_LOG_SIZE) t_fail(s, MR_FAIL_LOG_SIZE);
+    if (disconnect) {
+      t_connect(s, victim);
+      t_one(s, t_entry(s), n, 1);
+      leader1 = t_check_one_leader(s);
+    }
+    if (crash) {
+      t_start1(s, victim);
+      t_connect(s, victim);
+      t_one(s, t_entry(s), n, 1);
+      leader1 = t_check_one_leader(s);
+    }
+  }
+  t_end(s);
+}
+
+static int run_scenario(OSim* s) {
+  switch (s->scenario) {
+    case MR_SCN_INITIAL_ELECTION_2A: scn_initial_election(s); break;
+    case MR_SCN_REELECTION_2A: scn_reelection(s); break;
+    case MR_SCN_MANY_ELECTION_2A: scn_many_election(s); break;
+    case MR_SCN_BASIC_AGREE_2B: scn_basic_agree(s); break;
+    case MR_SCN_FAIL_AGREE_2B: scn_fail_agree(s); break;
+    case MR_SCN_FAIL_NO_AGREE_2B: scn_fail_no_agree(s); break;
+    case MR_SCN_CONCURRENT_STARTS_2B: scn_concurrent_starts(s); break;
+    case MR_SCN_REJOIN_2B: scn_rejoin(s); break;
+    case MR_SCN_BACKUP_2B: scn_backup(s); break;
+    case MR_SCN_COUNT_2B: scn_count(s); break;
+    case MR_SCN_PERSIST1_2C: scn_persist1(s); break;
+    case MR_SCN_PERSIST2_2C: scn_persist2(s); break;
+    case MR_SCN_PERSIST3_2C: scn_persist3(s); break;
+    case MR_SCN_FIGURE_8_2C:
+    case MR_SCN_FIGURE_8_UNRELIABLE_CRASH: scn_figure_8(s); break;
+    case MR_SCN_FIGURE_8_UNRELIABLE_2C: scn_figure_8_unreliable(s); break;
+    case MR_SCN_SNAPSHOT_BASIC_2D: scn_snap_common(s, 0, 1, 0); break;
+    case MR_SCN_SNAPSHOT_INSTALL_2D: scn_snap_common(s, 1, 1, 0); break;
+    case MR_SCN_SNAPSHOT_INSTALL_UNRELIABLE_2D: scn_snap_common(s, 1, 0, 0); break;
+    case MR_SCN_SNAPSHOT_INSTALL_CRASH_2D: scn_snap_common(s, 0, 1, 1); break;
+    case MR_SCN_SNAPSHOT_INSTALL_UNRELIABLE_CRASH_2D: scn_snap_common(s, 0, 0, 1); break;
+    default: return -1;
+  }
+  return 0;
+}
+
+/* ------------------------------------------------------------------ */
+/* seed loop                                                            */
+/* ------------------------------------------------------------------ */
+static int sim_alloc(OSim* s, const mr_cfg* cfg) {
+  memset(s, 0, sizeof *s);
+  s->cfg = *cfg;
+  if (cfg->n_nodes < 3 || cfg->n_nodes > MR_MAX_NODES) return -1;
+  if (cfg->log_cap < 16 || (cfg->log_cap & (cfg->log_cap - 1))) return -1;
+  if (cfg->msg_slots < 1 || cfg->msg_slots > MR_MAX_MSG_SLOTS) return -1;
+  if (cfg->ae_max < 1 || cfg->ae_max > MR_MAX_AE) return -1;
+  if (cfg->apply_cap < 16) return -1;
+  for (uint32_t i = 0; i < cfg->n_nodes; i++) {
+    s->nd[i].lterm = (uint32_t*)malloc(cfg->log_cap * sizeof(uint32_t));
+    s->nd[i].lval = (uint64_t*)malloc(cfg->log_cap * sizeof(uint64_t));
+  }
+  s->mask = (uint8_t*)malloc(cfg->apply_cap);
+  s->sval = (uint64_t*)malloc(cfg->apply_cap * sizeof(uint64_t));
+  return 0;
+}
+
+static void sim_free(OSim* s) {
+  for (uint32_t i = 0; i < MR_MAX_NODES; i++) { free(s->nd[i].lterm); free(s->nd[i].lval); }
+  free(s->mask); free(s->sval); free(s->heap);
+}
+
+static void sim_reset(OSim* s, uint64_t cluster) {
+  uint64_t seed = s->cfg.seed_base + cluster;
+  s->key[0] = (uint32_t)seed; s->key[1] = (uint32_t)(seed >> 32);
+  s->n = s->cfg.n_nodes; s->now = 0; s->scenario = s->cfg.scenario;
+  s->null_raft = (s->cfg.flags & MR_F_NULL_RAFT) ? 1 : 0;
+  s->snapshot_mode = 0;
+  t_set_unreliable(s, 0);
+  for (uint32_t i = 0; i < MR_MAX_NODES; i++) {
+    ONode* d = &s->nd[i];
+    uint32_t* lt = d->lterm; uint64_t* lv = d->lval;
+    memset(d, 0, sizeof *d);
+    d->lterm = lt; d->lval = lv;
+    d->voted = -1;
+  }
+  s->n_free = s->cfg.msg_slots;
+  for (uint32_t i = 0; i < s->n_free; i++) s->free_stack[i] = s->n_free - 1 - i;
+  s->inflight = 0; s->heap_n = 0; s->t_ctr = 0;
+  memset(s->mask, 0, s->cfg.apply_cap);
+  for (uint32_t i = 0; i < MR_MAX_NODES; i++) s->slen[i] = 1;
+  memset(&s->r, 0, sizeof s->r);
+  s->r.digest = 0xCBF29CE484222325ull;
+  s->n_trace = 0;
+}
+
+static void sim_run(OSim* s, uint64_t cluster) {
+  sim_reset(s, cluster);
+  if (setjmp(s->jb) == 0) {
+    count_event(s); /* the tester's first wake-up at t = 0 */
+    s->r.ev_tester++;
+    if (run_scenario(s) != 0) t_fail(s, MR_FAIL_SIM_BAD_PROGRAM);
+  }
+}
+
+int mro_run_cluster(const mr_cfg* cfg, uint64_t cluster, mro_result* out, mr_event* trace,
+                    size_t trace_cap, size_t* n_trace) {
+  OSim* s = (OSim*)malloc(sizeof(OSim));
+  if (!s || sim_alloc(s, cfg) != 0) { free(s); return -1; }
+  s->trace = trace; s->trace_cap = trace_cap;
+  sim_run(s, cfg->cluster_base + cluster);
+  if (out) *out = s->r;
+  if (n_trace) *n_trace = s->n_trace;
+  sim_free(s);
+  free(s);
+  return 0;
+}
+
+static void acc(mro_result* a, const mro_result* b) {
+  a->events += b->events; a->ev_msg += b->ev_msg; a->ev_timer += b->ev_timer;
+  a->ev_tester += b->ev_tester; a->msgs_sent += b->msgs_sent; a->drop_clog += b->drop_clog;
+  a->drop_loss += b->drop_loss; a->drop_overflow += b->drop_overflow;
+  a->drop_deliver += b->drop_deliver; a->drop_stale += b->drop_stale;
+  a->elections += b->elections; a->leaders_elected += b->leaders_elected;
+  a->applies += b->applies; a->snapshots += b->snapshots; a->installs += b->installs;
+  a->entries_shipped += b->entries_shipped;
+  if (b->max_inflight > a->max_inflight) a->max_inflight = b->max_inflight;
+  if (b->max_log > a->max_log) a->max_log = b->max_log;
+  if (b->max_index > a->max_index) a->max_index = b->max_index;
+}
+
+int mro_run_batch(const mr_cfg* cfg, uint64_t first, uint64_t count, uint16_t* code,
+                  uint32_t* time_us, uint64_t* digest, mro_result* sum) {
+  OSim* s = (OSim*)malloc(sizeof(OSim));
+  if (!s || sim_alloc(s, cfg) != 0) { free(s); return -1; }
+  if (sum) memset(sum, 0, sizeof *sum);
+  for (uint64_t c = 0; c < count; c++) {
+    sim_run(s, cfg->cluster_base + first + c);
+    if (code) code[c] = (uint16_t)s->r.code;
+    if (time_us) time_us[c] = s->r.time_us;
+    if (digest) digest[c] = s->r.digest;
+    if (sum) acc(sum, &s->r);
+  }
+  sim_free(s);
+  free(s);
+  return 0;
+}
+
+/* ------------------------------------------------------------------ */
+/* names / defaults (mirrors mr_cfg_init of the product ABI)           */
+/* ------------------------------------------------------------------ */
+static const char* k_names[MR_SCN_COUNT_] = {
+    "", "initial_election_2a", "reelection_2a", "many_election_2a", "basic_agree_2b",
+    "fail_agree_2b", "fail_no_agree_2b", "concurrent_starts_2b", "rejoin_2b", "backup_2b",
+    "count_2b", "persist1_2c", "persist2_2c", "persist3_2c", "figure_8_2c",
+    "unreliable_agree_2c", "figure_8_unreliable_2c", "reliable_churn_2c",
+    "unreliable_churn_2c", "snapshot_basic_2d", "snapshot_install_2d",
+    "snapshot_install_unreliable_2d", "snapshot_install_crash_2d",
+    "snapshot_install_unreliable_crash_2d", "figure_8_unreliable_crash"};
+
+uint32_t mro_scenario_from_name(const char* name) {
+  for (uint32_t i = 1; i < MR_SCN_COUNT_; i++)
+    if (strcmp(name, k_names[i]) == 0) return i;
+  return 0;
+}
+
+int mro_cfg_init(mr_cfg* c, uint32_t scn) {
+  static const uint8_t k_n[MR_SCN_COUNT_] = {0, 3, 3, 7, 5, 3, 5, 3, 3, 5, 3, 3, 5, 3,
+                                             5, 5, 5, 5, 5, 3, 3, 3, 3, 3, 5};
+  if (scn == 0 || scn >= MR_SCN_COUNT_) return -1;
+  memset(c, 0, sizeof *c);
+  c->abi_version = MR_ABI_VERSION;
+  c->scenario = scn;
+  c->n_nodes = k_n[scn];
+  c->seed_base = 1629626496ull; /* README.md:48 */
+  c->n_clusters = 1;
+  c->log_cap = 2048;
+  c->apply_cap = 4096;
+  c->msg_slots = 32;
+  c->ae_max = 16;
+  c->hb_us = 50000;
+  c->elect_lo_us = 150000;
+  c->elect_hi_us = 300000;
+  c->max_events = 4u << 20;
+  c->trace_cap = 1u << 16;
+  return 0;
+}
+
+const char* mro_fail_message(uint32_t code) {
+  switch (code) {
+    case MR_PASS: return "ok";
+    case MR_FAIL_ONE_LEADER_NONE: return "expected one leader, got none";
+    case MR_FAIL_MULTI_LEADER_TERM: return "term has (>1) leaders";
+    case MR_FAIL_TERM_DISAGREE: return "servers disagree on term";
+    case MR_FAIL_UNEXPECTED_LEADER: return "expected no leader, but claims to be leader";
+    case MR_FAIL_WAIT_TOO_FEW: return "only decided for index; wanted more";
+    case MR_FAIL_ONE_NO_AGREEMENT: return "one() failed to reach agreement";
+    case MR_FAIL_TIMEOUT_120S: return "test took longer than 120 seconds";
+    case MR_FAIL_APPLY_MISMATCH: return "commit index mismatch between servers";
+    case MR_FAIL_APPLY_OUT_OF_ORDER: return "server apply out of order";
+    case MR_FAIL_UNWRAP_NONE: return "called `Option::unwrap()` on a `None` value";
+    case MR_FAIL_LOG_SIZE: return "log size too large";
+    case MR_FAIL_SIM_CAPACITY: return "simulator capacity exceeded";
+    case MR_FAIL_SIM_EVENT_LIMIT: return "simulator event limit exceeded";
+    default: return "scenario assertion failed";
+  }
+}
