@@ -1,0 +1,29 @@
+"""CLI: `python -m madraft_amd <test> [--clusters N] [--seed S]` — the batched
+analogue of `MADSIM_TEST_SEED=S MADSIM_TEST_NUM=N cargo test <test>`."""
+import argparse
+import json
+import time
+
+from . import sim
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("test")
+    ap.add_argument("--clusters", type=int, default=None, help="seeds (MADSIM_TEST_NUM)")
+    ap.add_argument("--seed", type=int, default=None, help="first seed (MADSIM_TEST_SEED)")
+    ap.add_argument("--nodes", type=int, default=None)
+    ap.add_argument("--iters", type=int, default=0)
+    ap.add_argument("--unreliable", action="store_true")
+    ap.add_argument("--null", action="store_true", help="skeleton node (never campaigns)")
+    a = ap.parse_args()
+    t0 = time.time()
+    code, _, _, cnt = sim.run_test(a.test, a.seed, a.clusters, nodes=a.nodes, iters=a.iters,
+                                   unreliable=a.unreliable, null_raft=a.null)
+    cnt["wall_s"] = time.time() - t0
+    print(json.dumps(cnt))
+    raise SystemExit(0 if cnt["failed"] == 0 else 1)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,91 @@
+"""ctypes mirror of include/madraft_sim.h (structs, enums, numpy trace dtype).
+
+Plain data definitions only; loading a library is done by madraft_amd.sim
+(the HIP product) or by the tests (the CPU oracle).
+"""
+import ctypes as C
+
+import numpy as np
+
+MR_ABI_VERSION = 1
+MR_MAX_NODES = 8
+MR_RUNNING = 0xFFFF
+MR_PASS = 0
+
+MR_F_UNRELIABLE = 0x1
+MR_F_NULL_RAFT = 0x2
+MR_F_TRACE = 0x4
+
+README_SEED = 1629626496  # /root/reference/README.md:48
+
+# enum mr_scenario, in header order (tests.rs names)
+SCENARIOS = [
+    "", "initial_election_2a", "reelection_2a", "many_election_2a", "basic_agree_2b",
+    "fail_agree_2b", "fail_no_agree_2b", "concurrent_starts_2b", "rejoin_2b", "backup_2b",
+    "count_2b", "persist1_2c", "persist2_2c", "persist3_2c", "figure_8_2c",
+    "unreliable_agree_2c", "figure_8_unreliable_2c", "reliable_churn_2c",
+    "unreliable_churn_2c", "snapshot_basic_2d", "snapshot_install_2d",
+    "snapshot_install_unreliable_2d", "snapshot_install_crash_2d",
+    "snapshot_install_unreliable_crash_2d", "figure_8_unreliable_crash",
+]
+SCENARIO_ID = {n: i for i, n in enumerate(SCENARIOS) if n}
+# tests that still need multi-threaded tester programs (spawn_local); not built yet
+UNSUPPORTED = {"unreliable_agree_2c", "reliable_churn_2c", "unreliable_churn_2c"}
+
+FAIL_NAMES = {
+    0: "PASS", 1: "ONE_LEADER_NONE", 2: "MULTI_LEADER_TERM", 3: "TERM_DISAGREE",
+    4: "UNEXPECTED_LEADER", 5: "WAIT_TOO_FEW", 6: "ONE_NO_AGREEMENT", 7: "TIMEOUT_120S",
+    8: "APPLY_MISMATCH", 9: "APPLY_OUT_OF_ORDER", 10: "COMMIT_MISMATCH", 11: "UNWRAP_NONE",
+    12: "LOG_SIZE", 13: "BASIC_PRECOMMIT", 14: "BASIC_INDEX", 15: "LEADER_REJECTED",
+    16: "EXPECTED_INDEX2", 17: "NO_MAJORITY_COMMIT", 18: "UNEXPECTED_INDEX", 19: "CMD_MISSING",
+    20: "TERM_CHANGED", 21: "RPC_INITIAL", 22: "START_FAILED", 23: "WRONG_VALUE",
+    24: "RPC_TOO_MANY", 25: "RPC_IDLE", 26: "CHURN_VALUE", 60: "SIM_CAPACITY",
+    61: "SIM_EVENT_LIMIT", 62: "SIM_BAD_PROGRAM", 0xFFFF: "RUNNING",
+}
+
+
+class MrCfg(C.Structure):
+    _fields_ = [
+        ("abi_version", C.c_uint32), ("scenario", C.c_uint32), ("n_nodes", C.c_uint32),
+        ("flags", C.c_uint32), ("seed_base", C.c_uint64), ("cluster_base", C.c_uint64),
+        ("n_clusters", C.c_uint64), ("iters", C.c_uint32), ("log_cap", C.c_uint32),
+        ("apply_cap", C.c_uint32), ("msg_slots", C.c_uint32), ("ae_max", C.c_uint32),
+        ("hb_us", C.c_uint32), ("elect_lo_us", C.c_uint32), ("elect_hi_us", C.c_uint32),
+        ("max_events", C.c_uint32), ("trace_clusters", C.c_uint32), ("trace_cap", C.c_uint32),
+        ("device", C.c_int32), ("reserved", C.c_uint32 * 6),
+    ]
+
+
+class MrCounters(C.Structure):
+    _fields_ = [(n, C.c_uint64) for n in (
+        "clusters", "done", "passed", "failed", "events", "ev_msg", "ev_timer", "ev_tester",
+        "msgs_sent", "drop_clog", "drop_loss", "drop_overflow", "drop_deliver", "drop_stale",
+        "elections", "leaders_elected", "applies", "snapshots", "installs", "entries_shipped",
+        "virt_time_us", "max_inflight", "max_log", "max_index", "first_fail_cluster",
+        "first_fail_code")] + [("fail_hist", C.c_uint64 * 64)]
+
+    def to_dict(self):
+        d = {n: getattr(self, n) for n, _ in self._fields_ if n != "fail_hist"}
+        d["fail_hist"] = {FAIL_NAMES.get(i, str(i)): int(v)
+                          for i, v in enumerate(self.fail_hist) if v}
+        return d
+
+
+class MrRunStats(C.Structure):
+    _fields_ = [("launches", C.c_uint64), ("kernel_ms", C.c_double), ("wall_ms", C.c_double),
+                ("events", C.c_uint64), ("remaining", C.c_uint64)]
+
+
+EVENT_DTYPE = np.dtype([
+    ("time_us", "<u4"), ("cls", "u1"), ("kind", "u1"), ("node", "u1"), ("role", "u1"),
+    ("aux", "<u4"), ("term", "<u4"), ("commit", "<u4"), ("applied", "<u4"), ("last", "<u4"),
+    ("snap", "<u4"),
+])
+assert EVENT_DTYPE.itemsize == 32
+
+# symbols the product library exports (include/madraft_sim.h)
+EXPORTS = [
+    "mr_last_error", "mr_fail_message", "mr_scenario_name", "mr_scenario_from_name",
+    "mr_cfg_init", "mr_batch_create", "mr_batch_reset", "mr_batch_run", "mr_batch_verdicts",
+    "mr_batch_counters", "mr_trace_get", "mr_batch_destroy",
+]

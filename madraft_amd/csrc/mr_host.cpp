@@ -1,0 +1,375 @@
+// mr_host.cpp — C ABI of include/madraft_sim.h on one MI355X: allocates the
+// cluster-minor SoA of mr_dev.h in HBM (sized for the config, hundreds of
+// GB fit on a 288 GB part), builds the scenario program, and drives the
+// step kernel in bounded launches on the batch's own HIP stream, timing each
+// launch with HIP events on that stream.
+#include <hip/hip_runtime.h>
+
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "mr_dev.h"
+
+namespace mr {
+bool build_program(const mr_cfg& cfg, std::vector<uint64_t>& out);
+hipError_t launch_step(const Dev& D, uint32_t budget, hipStream_t s);
+hipError_t launch_reset(const Dev& D, hipStream_t s);
+hipError_t launch_reduce(const Dev& D, unsigned long long* out, uint64_t cluster_base,
+                         hipStream_t s);
+}  // namespace mr
+
+using namespace mr;
+
+namespace {
+thread_local std::string g_err;
+
+int set_err(const std::string& s) {
+  g_err = s;
+  return -1;
+}
+#define HIPCHK(expr)                                                                  \
+  do {                                                                                \
+    hipError_t e_ = (expr);                                                           \
+    if (e_ != hipSuccess)                                                             \
+      return set_err(std::string(#expr) + ": " + hipGetErrorString(e_));              \
+  } while (0)
+
+const char* k_names[MR_SCN_COUNT_] = {
+    "", "initial_election_2a", "reelection_2a", "many_election_2a", "basic_agree_2b",
+    "fail_agree_2b", "fail_no_agree_2b", "concurrent_starts_2b", "rejoin_2b", "backup_2b",
+    "count_2b", "persist1_2c", "persist2_2c", "persist3_2c", "figure_8_2c",
+    "unreliable_agree_2c", "figure_8_unreliable_2c", "reliable_churn_2c",
+    "unreliable_churn_2c", "snapshot_basic_2d", "snapshot_install_2d",
+    "snapshot_install_unreliable_2d", "snapshot_install_crash_2d",
+    "snapshot_install_unreliable_crash_2d", "figure_8_unreliable_crash"};
+// servers per test (tests.rs `let servers = ..`)
+const uint8_t k_nodes[MR_SCN_COUNT_] = {0, 3, 3, 7, 5, 3, 5, 3, 3, 5, 3, 3, 5, 3,
+                                        5, 5, 5, 5, 5, 3, 3, 3, 3, 3, 5};
+
+constexpr size_t RED_N = CNT__N + 8 + 64;  // reduce_kernel output slots
+}  // namespace
+
+struct mr_batch {
+  mr_cfg cfg;
+  Dev D;
+  void* base = nullptr;
+  size_t bytes = 0;
+  uint64_t* prog = nullptr;
+  unsigned long long* red = nullptr;
+  uint32_t* h_remaining = nullptr;
+  hipStream_t stream = nullptr;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  uint32_t budget = 2048;
+};
+
+extern "C" {
+
+const char* mr_last_error(void) { return g_err.c_str(); }
+
+const char* mr_scenario_name(uint32_t s) { return (s > 0 && s < MR_SCN_COUNT_) ? k_names[s] : ""; }
+
+uint32_t mr_scenario_from_name(const char* name) {
+  if (!name) return 0;
+  for (uint32_t i = 1; i < MR_SCN_COUNT_; i++)
+    if (std::strcmp(name, k_names[i]) == 0) return i;
+  return 0;
+}
+
+const char* mr_fail_message(uint32_t code) {
+  switch (code) {
+    case MR_PASS: return "ok";
+    case MR_FAIL_ONE_LEADER_NONE: return "expected one leader, got none";
+    case MR_FAIL_MULTI_LEADER_TERM: return "term has (>1) leaders";
+    case MR_FAIL_TERM_DISAGREE: return "servers disagree on term";
+    case MR_FAIL_UNEXPECTED_LEADER: return "expected no leader, but claims to be leader";
+    case MR_FAIL_WAIT_TOO_FEW: return "only decided for index; wanted more";
+    case MR_FAIL_ONE_NO_AGREEMENT: return "one() failed to reach agreement";
+    case MR_FAIL_TIMEOUT_120S: return "test took longer than 120 seconds";
+    case MR_FAIL_APPLY_MISMATCH: return "commit index mismatch between servers";
+    case MR_FAIL_APPLY_OUT_OF_ORDER: return "server apply out of order";
+    case MR_FAIL_COMMIT_MISMATCH: return "committed values do not match";
+    case MR_FAIL_UNWRAP_NONE: return "called `Option::unwrap()` on a `None` value";
+    case MR_FAIL_LOG_SIZE: return "log size too large";
+    case MR_FAIL_BASIC_PRECOMMIT: return "some have committed before start()";
+    case MR_FAIL_BASIC_INDEX: return "got index but expected another";
+    case MR_FAIL_LEADER_REJECTED: return "leader rejected start";
+    case MR_FAIL_EXPECTED_INDEX2: return "expected index 2";
+    case MR_FAIL_NO_MAJORITY_COMMIT: return "committed but no majority";
+    case MR_FAIL_UNEXPECTED_INDEX: return "unexpected index";
+    case MR_FAIL_CMD_MISSING: return "cmd missing";
+    case MR_FAIL_TERM_CHANGED: return "term changed too often";
+    case MR_FAIL_RPC_INITIAL: return "too many or few RPCs to elect initial leader";
+    case MR_FAIL_START_FAILED: return "start failed";
+    case MR_FAIL_WRONG_VALUE: return "wrong value committed";
+    case MR_FAIL_RPC_TOO_MANY: return "too many RPCs for entries";
+    case MR_FAIL_RPC_IDLE: return "too many RPCs for 1 second of idleness";
+    case MR_FAIL_CHURN_VALUE: return "didn't find a value";
+    case MR_FAIL_SIM_CAPACITY: return "simulator capacity exceeded";
+    case MR_FAIL_SIM_EVENT_LIMIT: return "simulator event limit exceeded";
+    case MR_FAIL_SIM_BAD_PROGRAM: return "scenario program error";
+    case MR_RUNNING: return "running";
+    default: return "unknown";
+  }
+}
+
+int mr_cfg_init(mr_cfg* c, uint32_t scn) {
+  if (!c) return set_err("null cfg");
+  if (scn == 0 || scn >= MR_SCN_COUNT_) return set_err("unknown scenario");
+  std::memset(c, 0, sizeof *c);
+  c->abi_version = MR_ABI_VERSION;
+  c->scenario = scn;
+  c->n_nodes = k_nodes[scn];
+  c->seed_base = 1629626496ull;  // README.md:48
+  c->n_clusters = 1;
+  /* capacities sized from the oracle's maxima over 2000 seeds */
+  int fig8 = scn == MR_SCN_FIGURE_8_2C || scn == MR_SCN_FIGURE_8_UNRELIABLE_2C ||
+             scn == MR_SCN_FIGURE_8_UNRELIABLE_CRASH;
+  int snap = scn >= MR_SCN_SNAPSHOT_BASIC_2D && scn <= MR_SCN_SNAPSHOT_INSTALL_UNRELIABLE_CRASH_2D;
+  c->log_cap = fig8 ? 2048 : 256;
+  c->apply_cap = fig8 ? 2048 : (snap ? 1024 : 512);
+  c->msg_slots = 32;
+  c->ae_max = 16;
+  c->hb_us = 50000;
+  c->elect_lo_us = 150000;  // raft.rs:262
+  c->elect_hi_us = 300000;
+  c->max_events = 4u << 20;
+  c->trace_cap = 1u << 16;
+  return 0;
+}
+
+static int validate(const mr_cfg* c) {
+  if (!c) return set_err("null cfg");
+  if (c->abi_version != MR_ABI_VERSION) return set_err("abi_version mismatch");
+  if (c->scenario == 0 || c->scenario >= MR_SCN_COUNT_) return set_err("unknown scenario");
+  if (c->n_nodes < 3 || c->n_nodes > MR_MAX_NODES) return set_err("n_nodes must be 3..8");
+  if (c->n_clusters == 0 || c->n_clusters > (1ull << 31)) return set_err("bad n_clusters");
+  if (c->log_cap < 16 || (c->log_cap & (c->log_cap - 1))) return set_err("log_cap: power of 2 >= 16");
+  if (c->apply_cap < 16) return set_err("apply_cap too small");
+  if (c->msg_slots < 1 || c->msg_slots > MR_MAX_MSG_SLOTS) return set_err("msg_slots must be 1..64");
+  if (c->ae_max < 1 || c->ae_max > MR_MAX_AE) return set_err("ae_max must be 1..32");
+  if (c->elect_hi_us <= c->elect_lo_us || c->hb_us == 0) return set_err("bad timers");
+  if (c->max_events == 0) return set_err("max_events must be > 0");
+  if ((c->flags & MR_F_TRACE) && (c->trace_cap == 0 || c->trace_clusters > c->n_clusters))
+    return set_err("bad trace config");
+  return 0;
+}
+
+int mr_batch_create(const mr_cfg* cfg, mr_batch** out) {
+  if (!out) return set_err("null out");
+  *out = nullptr;
+  if (validate(cfg) != 0) return -1;
+  std::vector<uint64_t> prog;
+  if (!build_program(*cfg, prog))
+    return set_err(std::string("scenario has no GPU program yet: ") + k_names[cfg->scenario]);
+
+  mr_batch* b = new mr_batch();
+  b->cfg = *cfg;
+  Dev& D = b->D;
+  std::memset(&D, 0, sizeof D);
+  const uint64_t C = cfg->n_clusters, n = cfg->n_nodes, M = cfg->msg_slots, K = cfg->ae_max;
+  D.C = (uint32_t)C; D.n = (uint32_t)n; D.log_cap = cfg->log_cap; D.apply_cap = cfg->apply_cap;
+  D.M = (uint32_t)M; D.K = (uint32_t)K; D.hb = cfg->hb_us; D.elo = cfg->elect_lo_us;
+  D.ehi = cfg->elect_hi_us; D.max_events = cfg->max_events;
+  D.null_raft = (cfg->flags & MR_F_NULL_RAFT) ? 1u : 0u;
+  D.unrel_flag = (cfg->flags & MR_F_UNRELIABLE) ? 1u : 0u;
+  D.trace_clusters = (cfg->flags & MR_F_TRACE) ? cfg->trace_clusters : 0u;
+  D.trace_cap = cfg->trace_cap;
+  D.prog_len = (uint32_t)prog.size();
+  D.seed0 = cfg->seed_base + cfg->cluster_base;
+
+  // carve one allocation; every array 256-B aligned
+  struct Item { void** p; size_t bytes; };
+  std::vector<Item> items;
+  auto add = [&](auto** p, size_t count) {
+    items.push_back({reinterpret_cast<void**>(p), count * sizeof(**p)});
+  };
+  add(&D.code, C);
+  for (uint32_t** p : {&D.vtime, &D.now, &D.events, &D.msgs_sent, &D.inflight, &D.netmode,
+                       &D.t_ctr, &D.trace_n, &D.mslot})
+    add(p, C);
+  for (uint64_t** p : {&D.free_mask, &D.digest, &D.mmin}) add(p, C);
+  add(&D.cnt, (size_t)CNT__N * C);
+  for (uint32_t** p : {&D.nflags, &D.nterm, &D.ncommit, &D.napplied, &D.nlast, &D.nsnap,
+                       &D.nsnapt, &D.ntimer, &D.nectr, &D.nnctr, &D.slen})
+    add(p, n * C);
+  add(&D.nsnapv, n * C);
+  add(&D.nnext, n * n * C);
+  add(&D.nmatch, n * n * C);
+  add(&D.lterm, C * n * cfg->log_cap);
+  add(&D.lval, C * n * cfg->log_cap);
+  add(&D.mkey, M * C);
+  for (uint32_t** p : {&D.mhdr, &D.mterm, &D.ma, &D.mb, &D.mc}) add(p, M * C);
+  add(&D.mv, M * C);
+  add(&D.pterm, C * M * K);
+  add(&D.pval, C * M * K);
+  add(&D.smask, C * cfg->apply_cap);
+  add(&D.sval, C * cfg->apply_cap);
+  for (uint32_t** p : {&D.tpc, &D.twake, &D.tphase}) add(p, C);
+  add(&D.ts, (size_t)N_S * C);
+  add(&D.tr, (size_t)N_R * C);
+  add(&D.tv, (size_t)N_V * C);
+  add(&D.trace, (size_t)D.trace_clusters * D.trace_cap);
+  add(&D.remaining, 1);
+  size_t total = 0;
+  for (auto& it : items) total += (it.bytes + 255) & ~size_t(255);
+
+  hipError_t e = hipSetDevice(cfg->device);
+  if (e == hipSuccess) e = hipMalloc(&b->base, total);
+  if (e == hipSuccess) e = hipMalloc(&b->prog, prog.size() * sizeof(uint64_t));
+  if (e == hipSuccess) e = hipMalloc(&b->red, RED_N * sizeof(unsigned long long));
+  if (e == hipSuccess) e = hipHostMalloc(&b->h_remaining, sizeof(uint32_t));
+  if (e == hipSuccess) e = hipStreamCreateWithFlags(&b->stream, hipStreamNonBlocking);
+  if (e == hipSuccess) e = hipEventCreate(&b->ev0);
+  if (e == hipSuccess) e = hipEventCreate(&b->ev1);
+  if (e == hipSuccess)
+    e = hipMemcpy(b->prog, prog.data(), prog.size() * sizeof(uint64_t), hipMemcpyHostToDevice);
+  if (e != hipSuccess) {
+    std::string msg = std::string("allocation of ") + std::to_string(total) + " B failed: " +
+                      hipGetErrorString(e);
+    mr_batch_destroy(b);
+    return set_err(msg);
+  }
+  b->bytes = total;
+  char* p = static_cast<char*>(b->base);
+  for (auto& it : items) {
+    *it.p = p;
+    p += (it.bytes + 255) & ~size_t(255);
+  }
+  D.prog = b->prog;
+  if (const char* s = std::getenv("MR_STEP_BUDGET")) b->budget = (uint32_t)std::atoi(s);
+  if (b->budget == 0) b->budget = 2048;
+  if (mr_batch_reset(b, cfg->seed_base) != 0) {
+    std::string msg = g_err;
+    mr_batch_destroy(b);
+    return set_err(msg);
+  }
+  *out = b;
+  return 0;
+}
+
+int mr_batch_reset(mr_batch* b, uint64_t seed_base) {
+  if (!b) return set_err("null batch");
+  b->cfg.seed_base = seed_base;
+  b->D.seed0 = seed_base + b->cfg.cluster_base;
+  HIPCHK(hipSetDevice(b->cfg.device));
+  HIPCHK(hipMemsetAsync(b->D.smask, 0, (size_t)b->D.C * b->D.apply_cap, b->stream));
+  HIPCHK(launch_reset(b->D, b->stream));
+  HIPCHK(hipStreamSynchronize(b->stream));
+  return 0;
+}
+
+int mr_batch_run(mr_batch* b, uint64_t max_events_per_call, mr_run_stats* st) {
+  if (!b) return set_err("null batch");
+  HIPCHK(hipSetDevice(b->cfg.device));
+  auto t0 = std::chrono::steady_clock::now();
+  mr_run_stats s;
+  std::memset(&s, 0, sizeof s);
+  uint64_t done_events = 0;
+  for (;;) {
+    uint32_t budget = b->budget;
+    if (max_events_per_call) {
+      if (done_events >= max_events_per_call) break;
+      uint64_t left = max_events_per_call - done_events;
+      if (left < budget) budget = (uint32_t)left;
+    }
+    HIPCHK(hipMemsetAsync(b->D.remaining, 0, sizeof(uint32_t), b->stream));
+    HIPCHK(hipEventRecord(b->ev0, b->stream));
+    HIPCHK(launch_step(b->D, budget, b->stream));
+    HIPCHK(hipEventRecord(b->ev1, b->stream));
+    HIPCHK(hipMemcpyAsync(b->h_remaining, b->D.remaining, sizeof(uint32_t), hipMemcpyDeviceToHost,
+                          b->stream));
+    HIPCHK(hipStreamSynchronize(b->stream));
+    float ms = 0.f;
+    HIPCHK(hipEventElapsedTime(&ms, b->ev0, b->ev1));
+    s.kernel_ms += ms;
+    s.launches++;
+    done_events += budget;
+    s.remaining = *b->h_remaining;
+    if (s.remaining == 0) break;
+  }
+  s.wall_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  // events processed: sum of per-cluster event counters (cheap reduce)
+  mr_counters c;
+  if (mr_batch_counters(b, &c) != 0) return -1;
+  s.events = c.events;
+  if (st) *st = s;
+  return 0;
+}
+
+int mr_batch_verdicts(mr_batch* b, uint16_t* code, uint32_t* time_us, uint64_t* digest) {
+  if (!b) return set_err("null batch");
+  HIPCHK(hipSetDevice(b->cfg.device));
+  size_t C = b->D.C;
+  if (code) HIPCHK(hipMemcpyAsync(code, b->D.code, C * 2, hipMemcpyDeviceToHost, b->stream));
+  if (time_us) HIPCHK(hipMemcpyAsync(time_us, b->D.vtime, C * 4, hipMemcpyDeviceToHost, b->stream));
+  if (digest) HIPCHK(hipMemcpyAsync(digest, b->D.digest, C * 8, hipMemcpyDeviceToHost, b->stream));
+  HIPCHK(hipStreamSynchronize(b->stream));
+  return 0;
+}
+
+int mr_batch_counters(mr_batch* b, mr_counters* out) {
+  if (!b || !out) return set_err("null argument");
+  HIPCHK(hipSetDevice(b->cfg.device));
+  std::vector<unsigned long long> h(RED_N, 0);
+  h[CNT__N + 5] = ~0ull;
+  HIPCHK(hipMemcpyAsync(b->red, h.data(), RED_N * 8, hipMemcpyHostToDevice, b->stream));
+  HIPCHK(launch_reduce(b->D, b->red, b->cfg.cluster_base, b->stream));
+  HIPCHK(hipMemcpyAsync(h.data(), b->red, RED_N * 8, hipMemcpyDeviceToHost, b->stream));
+  HIPCHK(hipStreamSynchronize(b->stream));
+  std::memset(out, 0, sizeof *out);
+  out->clusters = b->D.C;
+  out->ev_msg = h[CNT_EV_MSG]; out->ev_timer = h[CNT_EV_TIMER]; out->ev_tester = h[CNT_EV_TESTER];
+  out->drop_clog = h[CNT_DROP_CLOG]; out->drop_loss = h[CNT_DROP_LOSS];
+  out->drop_overflow = h[CNT_DROP_OVERFLOW]; out->drop_deliver = h[CNT_DROP_DELIVER];
+  out->drop_stale = h[CNT_DROP_STALE]; out->elections = h[CNT_ELECTIONS];
+  out->leaders_elected = h[CNT_LEADERS]; out->applies = h[CNT_APPLIES];
+  out->snapshots = h[CNT_SNAPSHOTS]; out->installs = h[CNT_INSTALLS];
+  out->entries_shipped = h[CNT_SHIPPED]; out->max_inflight = h[CNT_MAX_INFLIGHT];
+  out->max_log = h[CNT_MAX_LOG]; out->max_index = h[CNT_MAX_INDEX];
+  out->events = h[CNT__N + 0]; out->msgs_sent = h[CNT__N + 1]; out->virt_time_us = h[CNT__N + 2];
+  out->done = h[CNT__N + 3]; out->passed = h[CNT__N + 4]; out->failed = out->done - out->passed;
+  out->first_fail_cluster = h[CNT__N + 5];
+  for (int i = 0; i < 64; i++) out->fail_hist[i] = h[CNT__N + 8 + i];
+  out->first_fail_code = 0;
+  if (out->first_fail_cluster != ~0ull) {
+    uint16_t code = 0;
+    size_t idx = out->first_fail_cluster - b->cfg.cluster_base;
+    HIPCHK(hipMemcpy(&code, b->D.code + idx, 2, hipMemcpyDeviceToHost));
+    out->first_fail_code = code;
+  }
+  return 0;
+}
+
+int mr_trace_get(mr_batch* b, uint32_t k, mr_event* out, size_t cap, size_t* n) {
+  if (!b || !out || !n) return set_err("null argument");
+  if (k >= b->D.trace_clusters) return set_err("cluster not traced");
+  HIPCHK(hipSetDevice(b->cfg.device));
+  uint32_t tn = 0;
+  HIPCHK(hipMemcpy(&tn, b->D.trace_n + k, 4, hipMemcpyDeviceToHost));
+  size_t m = tn < b->D.trace_cap ? tn : b->D.trace_cap;
+  if (m > cap) m = cap;
+  HIPCHK(hipMemcpy(out, b->D.trace + (size_t)k * b->D.trace_cap, m * sizeof(mr_event),
+                   hipMemcpyDeviceToHost));
+  *n = m;
+  return 0;
+}
+
+void mr_batch_destroy(mr_batch* b) {
+  if (!b) return;
+  (void)hipSetDevice(b->cfg.device);
+  if (b->stream) (void)hipStreamSynchronize(b->stream);
+  if (b->base) (void)hipFree(b->base);
+  if (b->prog) (void)hipFree(b->prog);
+  if (b->red) (void)hipFree(b->red);
+  if (b->h_remaining) (void)hipHostFree(b->h_remaining);
+  if (b->ev0) (void)hipEventDestroy(b->ev0);
+  if (b->ev1) (void)hipEventDestroy(b->ev1);
+  if (b->stream) (void)hipStreamDestroy(b->stream);
+  delete b;
+}
+
+}  // extern "C"

@@ -1178,8 +1178,12 @@ int mro_cfg_init(mr_cfg* c, uint32_t scn) {
   c->n_nodes = k_n[scn];
   c->seed_base = 1629626496ull; /* README.md:48 */
   c->n_clusters = 1;
-  c->log_cap = 2048;
-  c->apply_cap = 4096;
+  /* capacities sized from the oracle's maxima over 2000 seeds */
+  int fig8 = scn == MR_SCN_FIGURE_8_2C || scn == MR_SCN_FIGURE_8_UNRELIABLE_2C ||
+             scn == MR_SCN_FIGURE_8_UNRELIABLE_CRASH;
+  int snap = scn >= MR_SCN_SNAPSHOT_BASIC_2D && scn <= MR_SCN_SNAPSHOT_INSTALL_UNRELIABLE_CRASH_2D;
+  c->log_cap = fig8 ? 2048 : 256;
+  c->apply_cap = fig8 ? 2048 : (snap ? 1024 : 512);
   c->msg_slots = 32;
   c->ae_max = 16;
   c->hb_us = 50000;

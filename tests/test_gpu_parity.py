@@ -1,0 +1,125 @@
+"""GPU parity: the HIP step kernel (through the C ABI) against the CPU oracle.
+
+Bar (integer simulation): bit-exact. Per cluster the verdict code, verdict
+time and the FNV-1a digest of the full event trace must equal the oracle's;
+for traced clusters every 32-byte trace record (per-node term / role /
+commit / applied / last / snapshot index after every event) must be equal;
+the batch counters must equal the oracle's sums. At BASELINE sizes the
+oracle checks a seeded random subset of clusters, and size-independent
+properties cover the rest (every cluster reaches a verdict, verdicts are in
+the set the test can produce, counters are self-consistent).
+"""
+import numpy as np
+import pytest
+
+from madraft_amd import _abi
+
+pytestmark = pytest.mark.gpu
+
+SUPPORTED = [n for n in _abi.SCENARIOS if n and n not in _abi.UNSUPPORTED]
+COUNTER_KEYS = ["events", "ev_msg", "ev_timer", "ev_tester", "msgs_sent", "drop_clog",
+                "drop_loss", "drop_overflow", "drop_deliver", "drop_stale", "elections",
+                "leaders_elected", "applies", "snapshots", "installs", "entries_shipped",
+                "max_inflight", "max_log", "max_index"]
+
+
+def first_diff(a, b):
+    n = min(len(a), len(b))
+    for i in range(n):
+        if a[i] != b[i]:
+            return i, a[i], b[i]
+    return n, (a[n] if n < len(a) else None), (b[n] if n < len(b) else None)
+
+
+def compare(hip, oracle, test, clusters, traced=4, first=0, **kw):
+    with hip.Batch(test, clusters, trace_clusters=traced, cluster_base=first, **kw) as b:
+        st = b.run()
+        assert st["remaining"] == 0
+        code, t, dig = b.verdicts()
+        cnt = b.counters()
+        traces = [b.trace(k) for k in range(traced)]
+        cfg = b.cfg
+    ocode, ot, odig, osum = oracle.run_batch(cfg, 0, clusters)
+    for k in range(traced):
+        _, otr = oracle.run_cluster(cfg, k, trace_cap=int(cfg.trace_cap))
+        if not np.array_equal(traces[k], otr):
+            i, g, o = first_diff(traces[k], otr)
+            pytest.fail(f"{test} cluster {k}: trace differs at record {i}: gpu={g} oracle={o}")
+    bad = np.nonzero((code != ocode) | (t != ot) | (dig != odig))[0]
+    assert bad.size == 0, (f"{test}: {bad.size} clusters differ, first {bad[0]}: "
+                           f"gpu=({code[bad[0]]},{t[bad[0]]}) oracle=({ocode[bad[0]]},{ot[bad[0]]})")
+    for k in COUNTER_KEYS:
+        assert cnt[k] == osum[k], (test, k, cnt[k], osum[k])
+    assert cnt["done"] == clusters
+    return code, cnt
+
+
+@pytest.mark.parametrize("test", SUPPORTED)
+def test_scenario_bit_exact(hip, oracle, test):
+    code, _ = compare(hip, oracle, test, 256)
+    assert (code == 0).mean() > 0.95
+
+
+def test_null_node_kat(hip, oracle):
+    """Skeleton KAT on the GPU: README.md:44-48 verdict, same as the oracle."""
+    code, cnt = compare(hip, oracle, "initial_election_2a", 64, null_raft=True)
+    assert (code == 1).all() and cnt["msgs_sent"] == 0
+    code, cnt = compare(hip, oracle, "basic_agree_2b", 64, null_raft=True)
+    assert (code == 6).all()
+
+
+def test_fail_agree_5_unreliable(hip, oracle):
+    """BASELINE config 2 shape (5 nodes, message drop) at oracle-checkable size."""
+    compare(hip, oracle, "fail_agree_2b", 1024, nodes=5, unreliable=True)
+
+
+def test_snapshot_7_nodes(hip, oracle):
+    """BASELINE config 4 shape: 2D InstallSnapshot with partitions, 7 nodes."""
+    code, cnt = compare(hip, oracle, "snapshot_install_unreliable_2d", 256, nodes=7)
+    assert cnt["installs"] > 0 and cnt["snapshots"] > 0
+
+
+def test_sharded_cluster_base(hip, oracle):
+    """A shard (cluster_base != 0) computes the same seeds as the oracle's global ids."""
+    compare(hip, oracle, "figure_8_unreliable_2c", 128, traced=2, first=5000)
+
+
+def test_small_capacities_fail_identically(hip, oracle):
+    """Capacity limits are part of the semantics: tiny rings / slots give the
+    same SIM_CAPACITY / overflow verdicts on both sides."""
+    compare(hip, oracle, "figure_8_unreliable_2c", 128, log_cap=64, msg_slots=6, ae_max=2)
+
+
+def test_step_budget_independence(hip):
+    """Results do not depend on how many events one launch processes."""
+    with hip.Batch("figure_8_unreliable_2c", 512) as b:
+        b.run()
+        ref = b.verdicts()
+        b.reset(b.cfg.seed_base)
+        while b.run(max_events=97)["remaining"]:
+            pass
+        got = b.verdicts()
+    for a, c in zip(ref, got):
+        assert np.array_equal(a, c)
+
+
+@pytest.mark.parametrize("test,clusters,kw", [
+    ("fail_agree_2b", 65536, dict(nodes=5, unreliable=True)),     # BASELINE config 2
+    ("figure_8_unreliable_2c", 131072, {}),                        # config 3, one GPU's shard
+    ("snapshot_install_unreliable_2d", 65536, dict(nodes=7)),      # config 4 shape
+])
+def test_baseline_sizes(hip, oracle, test, clusters, kw):
+    with hip.Batch(test, clusters, **kw) as b:
+        st = b.run()
+        code, t, dig = b.verdicts()
+        cnt = b.counters()
+        cfg = b.cfg
+    assert st["remaining"] == 0 and cnt["done"] == clusters
+    assert (code != _abi.MR_RUNNING).all()
+    assert cnt["events"] == cnt["ev_msg"] + cnt["ev_timer"] + cnt["ev_tester"]
+    assert sum(cnt["fail_hist"].values()) == clusters
+    assert cnt["drop_overflow"] == 0 and (code < 60).all()  # no simulator limits hit
+    rng = np.random.default_rng(clusters)
+    for k in rng.choice(clusters, 48, replace=False):
+        oc, ot, od, _ = oracle.run_batch(cfg, int(k), 1)
+        assert (oc[0], ot[0], od[0]) == (code[k], t[k], dig[k]), (test, int(k))

@@ -1,0 +1,121 @@
+"""CPU: pin the oracle (known answers) before trusting it as the parity checker.
+
+What pins it (MadSim RNG-stream parity itself is unpinned):
+  * Philox4x32-10 known-answer vectors (Random123 kat_vectors);
+  * skeleton-verdict KATs: with the as-shipped node (raft.rs todo!(), never
+    campaigns) the reference tester panics exactly as README.md:44-48 shows;
+  * the reference tests' own assertions: every in-scope test passes on its
+    seeds with the oracle's Raft (basic_agree's index == 1,2,3, count_2b's
+    RPC budgets, snap_common's log-size bound, ...);
+  * determinism (MADSIM_TEST_CHECK_DETERMINISTIC, README.md:81-85);
+  * committed golden fixtures (tests/golden/, made by tests/golden/make_golden.py).
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from madraft_amd import _abi
+
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden", "oracle_golden.json")
+
+SUPPORTED = [n for n in _abi.SCENARIOS if n and n not in _abi.UNSUPPORTED]
+
+
+def test_philox_known_answers(oracle):
+    # Random123 kat_vectors, philox4x32 10 rounds
+    assert oracle.philox([0, 0, 0, 0], [0, 0]) == [0x6627E8D5, 0xE169C58D, 0xBC57AC4C, 0x9B00DBD8]
+    f = 0xFFFFFFFF
+    assert oracle.philox([f, f, f, f], [f, f]) == [0x408F276D, 0x41C83B0E, 0xA20BC7C6, 0x6D5451FD]
+    assert oracle.philox([0x243F6A88, 0x85A308D3, 0x13198A2E, 0x03707344],
+                         [0xA4093822, 0x299F31D0]) == [0xD16CFE09, 0x94FDCCEB, 0x5001E420,
+                                                      0x24126EA1]
+
+
+def test_skeleton_initial_election_panics_like_readme(oracle):
+    """README.md:44-48: initial_election_2a on the skeleton panics at tester.rs:91
+    'expected one leader, got none' after check_one_leader's 10 samples."""
+    cfg = oracle.cfg("initial_election_2a", flags=_abi.MR_F_NULL_RAFT)
+    r, tr = oracle.run_cluster(cfg, 0, trace_cap=64)
+    assert r["code"] == 1  # MR_FAIL_ONE_LEADER_NONE
+    # 10 sleeps of U[450, 550) ms (tester.rs:69)
+    assert 4_500_000 <= r["time_us"] < 5_500_000
+    assert r["msgs_sent"] == 0 and r["elections"] == 0
+    assert r["ev_tester"] == 11  # t = 0 plus 10 wake-ups
+    assert tr[-1]["cls"] == 3 and tr[-1]["kind"] == 1
+
+
+@pytest.mark.parametrize("test", ["basic_agree_2b", "fail_agree_2b", "figure_8_2c",
+                                  "figure_8_unreliable_2c", "snapshot_basic_2d"])
+def test_skeleton_one_fails_after_10s(oracle, test):
+    """tester.rs:216-262: with no leader, one() retries every 50 ms and panics
+    'failed to reach agreement' (tester.rs:261) once 10 s have elapsed."""
+    cfg = oracle.cfg(test, flags=_abi.MR_F_NULL_RAFT)
+    r, _ = oracle.run_cluster(cfg, 0)
+    assert r["code"] == 6  # MR_FAIL_ONE_NO_AGREEMENT
+    assert r["time_us"] == 10_000_000
+    assert r["ev_tester"] == 1 + 200
+
+
+@pytest.mark.parametrize("test", SUPPORTED)
+def test_reference_assertions_hold(oracle, test):
+    """Every in-scope reference test passes on 64 seeds: its own assertions
+    (tests.rs) and the tester's checks (tester.rs) hold for the oracle's Raft."""
+    cfg = oracle.cfg(test)
+    code, t, dig, s = oracle.run_batch(cfg, 0, 64)
+    assert (code == 0).all(), {int(c): int((code == c).sum()) for c in np.unique(code)}
+    assert (t <= 120_000_000).all()
+    assert s["drop_overflow"] == 0
+
+
+def test_count_2b_budgets(oracle):
+    """tests.rs:397-401,461-463,472-476 — RPC budgets are part of the verdict."""
+    cfg = oracle.cfg("count_2b")
+    code, _, _, s = oracle.run_batch(cfg, 0, 200)
+    assert (code == 0).all()
+
+
+def test_determinism(oracle):
+    """MADSIM_TEST_CHECK_DETERMINISTIC: the same seed twice gives identical traces."""
+    cfg = oracle.cfg("figure_8_unreliable_2c", iters=200)
+    a, ta = oracle.run_cluster(cfg, 7, trace_cap=100000)
+    b, tb = oracle.run_cluster(cfg, 7, trace_cap=100000)
+    assert a == b
+    assert np.array_equal(ta, tb)
+    c, _ = oracle.run_cluster(cfg, 8)
+    assert c["digest"] != a["digest"]
+
+
+def test_trace_digest_consistency(oracle):
+    """The digest is FNV-1a-64 over the 8 words of every trace record."""
+    cfg = oracle.cfg("initial_election_2a")
+    r, tr = oracle.run_cluster(cfg, 3, trace_cap=100000)
+    h = 0xCBF29CE484222325
+    for w in tr.view(np.uint32):
+        h = ((h ^ int(w)) * 0x100000001B3) & 0xFFFFFFFFFFFFFFFF
+    assert h == r["digest"]
+    assert tr["time_us"].tolist() == sorted(tr["time_us"].tolist())
+
+
+def test_unreliable_fail_agree_config(oracle):
+    """BASELINE config 2: fail_agree_2b with 5 nodes and message drop. one(.., false)
+    may legitimately miss its 2 s window under 10 % loss: verdicts are data."""
+    cfg = oracle.cfg("fail_agree_2b", n_nodes=5, flags=_abi.MR_F_UNRELIABLE)
+    code, _, _, s = oracle.run_batch(cfg, 0, 300)
+    assert set(np.unique(code).tolist()) <= {0, 6}
+    assert (code == 0).mean() > 0.9
+    assert s["drop_loss"] > 0
+
+
+def test_golden_fixtures(oracle):
+    """Committed oracle outputs (tests/golden/make_golden.py) still reproduce."""
+    with open(GOLDEN) as f:
+        gold = json.load(f)
+    for case in gold["cases"]:
+        cfg = oracle.cfg(case["test"], **case["cfg"])
+        code, t, dig, s = oracle.run_batch(cfg, case["first"], case["count"])
+        assert code.tolist() == case["code"], case["test"]
+        assert t.tolist() == case["time_us"], case["test"]
+        assert [format(int(d), "016x") for d in dig] == case["digest"], case["test"]
+        assert s["events"] == case["events"], case["test"]
