@@ -1,0 +1,62 @@
+"""Multi-GPU: clusters shard across ranks; one collective at the end.
+
+Clusters (seeds) are independent — there is no inter-cluster traffic in any
+in-scope test — so rank r of W owns the contiguous global
+cluster range shard(total, W, r) and runs the identical kernel on it. Seeds
+derive from global cluster ids, so results do not depend on W. The only
+collective is one all-reduce of the batch counters at the end: sum for
+counts, max for maxima, min for the first failing global cluster id. With
+backend "nccl" that all-reduce is RCCL over xGMI; a few hundred bytes,
+latency-bound. Tests run the same code with gloo on CPU.
+"""
+import torch
+import torch.distributed as dist
+
+from ._abi import FAIL_NAMES
+
+SUM_KEYS = ["clusters", "done", "passed", "failed", "events", "ev_msg", "ev_timer", "ev_tester",
+            "msgs_sent", "drop_clog", "drop_loss", "drop_overflow", "drop_deliver", "drop_stale",
+            "elections", "leaders_elected", "applies", "snapshots", "installs",
+            "entries_shipped", "virt_time_us"]
+MAX_KEYS = ["max_inflight", "max_log", "max_index"]
+NO_FAIL = (1 << 63) - 1
+
+
+def shard(total, world, rank):
+    """(cluster_base, count) of `rank`'s contiguous share of `total` clusters."""
+    q, r = divmod(int(total), int(world))
+    base = rank * q + min(rank, r)
+    return base, q + (1 if rank < r else 0)
+
+
+def allreduce_counters(c, device=None, group=None):
+    """All-reduce a counters dict (madraft_amd.sim.Batch.counters()) across ranks."""
+    dev = device if device is not None else torch.device("cpu")
+    s = torch.tensor([int(c[k]) for k in SUM_KEYS], dtype=torch.int64, device=dev)
+    m = torch.tensor([int(c[k]) for k in MAX_KEYS], dtype=torch.int64, device=dev)
+    ff = int(c.get("first_fail_cluster", NO_FAIL))
+    ff = NO_FAIL if ff >= NO_FAIL else ff
+    f = torch.tensor([ff], dtype=torch.int64, device=dev)
+    names = sorted(FAIL_NAMES.items())
+    code_of = {v: k for k, v in names}
+    h = torch.zeros(len(names), dtype=torch.int64, device=dev)
+    for name, v in c.get("fail_hist", {}).items():
+        h[[k for k, _ in names].index(code_of[name])] = int(v)
+    s = torch.cat([s, h])
+    dist.all_reduce(s, op=dist.ReduceOp.SUM, group=group)
+    dist.all_reduce(m, op=dist.ReduceOp.MAX, group=group)
+    dist.all_reduce(f, op=dist.ReduceOp.MIN, group=group)
+    out = dict(c)
+    sl = s.tolist()
+    out["fail_hist"] = {name: int(v) for (_, name), v in zip(names, sl[len(SUM_KEYS):]) if v}
+    out.update({k: int(v) for k, v in zip(SUM_KEYS, sl)})
+    out.update({k: int(v) for k, v in zip(MAX_KEYS, m.tolist())})
+    out["first_fail_cluster"] = None if int(f.item()) == NO_FAIL else int(f.item())
+    return out
+
+
+def allreduce_max(x, device=None, group=None):
+    t = torch.tensor([float(x)], dtype=torch.float64,
+                     device=device if device is not None else torch.device("cpu"))
+    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+    return float(t.item())
