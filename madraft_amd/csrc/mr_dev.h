@@ -1,14 +1,15 @@
-// mr_dev.h — device state layout and tester ISA shared by the HIP kernels
-// (mr_kernel.hip) and the C++ batch driver (mr_host.cpp).
+// mr_dev.h — device state layout shared by the HIP kernels (mr_kernel.hip)
+// and the C++ batch driver (mr_host.cpp).
 //
-// Layout: one thread simulates one cluster. Every per-cluster scalar is an
-// array indexed [field][cluster] (cluster-minor), so the 64 lanes of a wave,
-// which hold 64 consecutive clusters, touch 64 consecutive words of a field:
-// one or two 256-B segments per wave instruction. Per-node fields are
-// [node][cluster]; next/match are [(leader*n + peer)][cluster]. Data a lane
-// walks through by index (Raft log rings, message payloads, the tester's
-// apply checker) is cluster-major so each lane's walk stays in its own
-// cache lines.
+// Layout: one lane simulates one cluster. State is grouped into a few
+// field-indexed matrices, each [field][...][cluster] (cluster-minor), so the
+// 64 lanes of a wave — 64 consecutive clusters — touch 64 consecutive words
+// of a field (one or two 256-B segments per wave instruction), and the
+// kernel needs one base pointer per matrix instead of one per field (the
+// per-field pointers alone overflowed the 102-SGPR budget). Index math is
+// 32-bit (checked at batch creation). Data a lane walks by index — Raft log
+// rings, message payloads, the tester's apply checker — is cluster-major so
+// each lane's walk stays in its own cache lines (64-bit offsets).
 #pragma once
 #include <stdint.h>
 
@@ -22,105 +23,57 @@ enum : uint32_t { R_F = 0, R_C = 1, R_L = 2, R_DOWN = 3 };
 enum : uint32_t { M_RV_REQ = 1, M_RV_REP, M_AE_REQ, M_AE_REP, M_IS_REQ, M_IS_REP };
 enum : uint32_t { ST_TESTER = 1, ST_ELECT = 2, ST_NET = 3 };
 
-// per-cluster u32 counters, [CNT_*][cluster]
+// per-cluster u32 counters (part of cs32); the last three are maxima
 enum : uint32_t {
   CNT_EV_MSG, CNT_EV_TIMER, CNT_EV_TESTER, CNT_DROP_CLOG, CNT_DROP_LOSS, CNT_DROP_OVERFLOW,
   CNT_DROP_DELIVER, CNT_DROP_STALE, CNT_ELECTIONS, CNT_LEADERS, CNT_APPLIES, CNT_SNAPSHOTS,
   CNT_INSTALLS, CNT_SHIPPED, CNT_MAX_INFLIGHT, CNT_MAX_LOG, CNT_MAX_INDEX, CNT__N
 };
 
-// ---- tester ISA: 64-bit instructions  op[0:8) a[8:16) b[16:24) c[24:32) imm[32:64)
+// tester coroutine frame (per cluster): program counter, script locals,
+// helper frame of the multi-event tester calls (one / wait / check_one_leader)
+constexpr uint32_t T_NL = 8;   // u32 script locals
+constexpr uint32_t T_NH = 5;   // u32 helper frame
+constexpr uint32_t T_NV = 16;  // u64 script arrays (count_2b / concurrent_starts)
+
+// cs32 [CS__N][C]: per-cluster u32 scalars
 enum : uint32_t {
-  OP_NOP = 0,
-  OP_NEW,            // a = snapshot mode: RaftTester::new / new_with_snapshot
-  OP_SET_UNREL,      // a = flag: set_unreliable
-  OP_END,            // end(): check_timeout, pass
-  OP_FAIL,           // imm = fail code
-  OP_SLEEP,          // imm = us
-  OP_SLEEP_FIG8,     // tests.rs:631-636: gen_bool(0.1) ? U[0,500ms) : U[0,13ms)
-  OP_CHECK_ONE_LEADER,  // r[a] = leader                       (multi-event)
-  OP_CHECK_TERMS,    // r[a] = term
-  OP_CHECK_NO_LEADER,
-  OP_ONE,            // r[a] = one(v[b&15], expected(c), retry = b>>7)  (multi-event)
-  OP_WAIT,           // wait(r[a], n(c), start_term = b==0xFF ? None : r[b]) -> r31 some, v15
-  OP_NCOMMITTED,     // n_committed(r[a]) -> r31 count, v15 value
-  OP_START,          // start((r[a]+b)%n, v[c]) -> r31 ok, r30 index, r29 term
-  OP_ENTRY,          // v[a] = gen_entry
-  OP_LDV,            // v[a] = imm
-  OP_VLDR,           // v[a] = r[b]
-  OP_RAND,           // r[a] = U[0, c ? n : imm)
-  OP_CONNECT,        // node (r[a]+b)%n
-  OP_DISCONNECT,
-  OP_CRASH,
-  OP_START1,
-  OP_CONNECT_ALL,
-  OP_DISCONNECT_ALL,
-  OP_IS_STARTED,     // r31 = is_started((r[a]+b)%n)
-  OP_IS_CONNECTED,   // r31 = is_connected((r[a]+b)%n)
-  OP_TERM,           // r[a] = term((r[b]+c)%n)   (unwrap)
-  OP_LOG_SIZE,       // r[a]
-  OP_RPC_TOTAL,      // r[a]
-  OP_MOVI,           // r[a] = imm
-  OP_MOVN,           // r[a] = n
-  OP_MOV,            // r[a] = r[b]
-  OP_ADDI,           // r[a] = r[b] + imm
-  OP_ADD,            // r[a] = r[b] + r[c]
-  OP_SUB,            // r[a] = r[b] - r[c]
-  OP_MODN,           // r[a] = (r[b] + imm) % n
-  OP_LT,             // r[a] = r[b] < r[c]
-  OP_LTI,            // r[a] = r[b] < imm
-  OP_LTN,            // r[a] = r[b] < n
-  OP_EQ,             // r[a] = r[b] == r[c]
-  OP_EQI,            // r[a] = r[b] == imm
-  OP_VEQ,            // r[a] = v[b] == v[c]
-  OP_RSETX,          // r[(r[a]+b)&31] = r[c]
-  OP_RGETX,          // r[a] = r[(r[b]+c)&31]
-  OP_VSETX,          // v[(r[a]+b)&15] = v[c]
-  OP_VGETX,          // v[a] = v[(r[b]+c)&15]
-  OP_JMP,            // pc = imm
-  OP_BRZ,            // if r[a] == 0: pc = imm
-  OP_BRNZ,           // if r[a] != 0: pc = imm
-  OP__N
+  CS_CODE, CS_VTIME, CS_NOW, CS_EVENTS, CS_MSGS, CS_INFLIGHT, CS_NETMODE, CS_TCTR, CS_TRACEN,
+  CS_MSLOT, CS_TPC, CS_TWAKE, CS_TRES, CS_TL, CS_TH = CS_TL + T_NL, CS_CNT = CS_TH + T_NH,
+  CS__N = CS_CNT + CNT__N
 };
-// expected-server operand: c < 128 -> c ; c >= 128 -> n - (c - 128)
-constexpr uint32_t EXP_N(uint32_t minus) { return 128u + minus; }
-constexpr uint32_t R_FLAG = 31, R_IDX = 30, R_TERM = 29;  // fixed result registers
-constexpr uint32_t V_RES = 15;
-constexpr uint32_t N_R = 32, N_V = 16, N_S = 6;  // tester registers / multi-event op scratch
+// cs64 [C64__N][C]: per-cluster u64 scalars
+enum : uint32_t { C64_FREE, C64_DIGEST, C64_MMIN, C64_THV, C64_TV, C64__N = C64_TV + T_NV };
+// nd32 [NF__N][n][C]: per-node u32 fields
+enum : uint32_t {
+  NF_FLAGS, NF_TERM, NF_COMMIT, NF_APPLIED, NF_LAST, NF_SNAP, NF_SNAPT, NF_TIMER, NF_ECTR,
+  NF_NCTR, NF_SLEN, NF__N
+};
+// pr32 [PF__N][n][n][C]: leader -> peer
+enum : uint32_t { PF_NEXT, PF_MATCH, PF__N };
+// ms32 [MF__N][M][C]: in-flight message fields; ms64 [2][M][C]: key, value
+enum : uint32_t { MF_HDR, MF_TERM, MF_A, MF_B, MF_C, MF__N };
+enum : uint32_t { M64_KEY, M64_V, M64__N };
 
 // ---- everything the kernels see (passed by value as a kernel argument)
 struct Dev {
   // config
   uint32_t C, n, log_cap, apply_cap, M, K, hb, elo, ehi, max_events;
-  uint32_t null_raft, unrel_flag, trace_clusters, trace_cap, prog_len, pad;
+  uint32_t null_raft, unrel_flag, trace_clusters, trace_cap, scenario, iters;
   uint64_t seed0;  // seed of cluster 0 = seed_base + cluster_base
-  const uint64_t* prog;
-  // cluster scalars [C]
-  uint16_t* code;
-  uint32_t *vtime, *now, *events, *msgs_sent, *inflight, *netmode, *t_ctr, *trace_n, *mslot;
-  uint64_t *free_mask, *digest, *mmin;
-  uint32_t* cnt;  // [CNT__N][C]
-  // nodes [n][C]
-  uint32_t *nflags, *nterm, *ncommit, *napplied, *nlast, *nsnap, *nsnapt, *ntimer, *nectr, *nnctr;
-  uint64_t* nsnapv;
-  uint32_t *nnext, *nmatch;  // [(d*n+p)][C]
-  uint32_t* lterm;           // [C][n][log_cap]
+  uint32_t* cs32;
+  uint64_t* cs64;
+  uint32_t* nd32;
+  uint64_t* nsnapv;  // [n][C]
+  uint32_t* pr32;
+  uint32_t* ms32;
+  uint64_t* ms64;
+  uint32_t* lterm;  // [C][n][log_cap]
   uint64_t* lval;
-  // messages [M][C]
-  uint64_t* mkey;
-  uint32_t *mhdr, *mterm, *ma, *mb, *mc;
-  uint64_t* mv;
   uint32_t* pterm;  // [C][M][K]
   uint64_t* pval;
-  // tester storage (tester.rs:366-428)
-  uint8_t* smask;  // [C][apply_cap]
+  uint8_t* smask;   // [C][apply_cap]   tester storage (tester.rs:366-428)
   uint64_t* sval;
-  uint32_t* slen;  // [n][C]
-  // tester interpreter
-  uint32_t *tpc, *twake, *tphase;
-  uint32_t* ts;  // [N_S][C]
-  uint32_t* tr;  // [N_R][C]
-  uint64_t* tv;  // [N_V][C]
   mr_event* trace;  // [trace_clusters][trace_cap]
   uint32_t* remaining;  // clusters without verdict after a step launch
 };

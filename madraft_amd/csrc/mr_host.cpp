@@ -1,8 +1,8 @@
 // mr_host.cpp — C ABI of include/madraft_sim.h on one MI355X: allocates the
 // cluster-minor SoA of mr_dev.h in HBM (sized for the config, hundreds of
-// GB fit on a 288 GB part), builds the scenario program, and drives the
-// step kernel in bounded launches on the batch's own HIP stream, timing each
-// launch with HIP events on that stream.
+// GB fit on a 288 GB part), and drives the step kernel in bounded launches
+// on the batch's own HIP stream, timing each launch with HIP events on that
+// stream.
 #include <hip/hip_runtime.h>
 
 #include <chrono>
@@ -15,7 +15,6 @@
 #include "mr_dev.h"
 
 namespace mr {
-bool build_program(const mr_cfg& cfg, std::vector<uint64_t>& out);
 hipError_t launch_step(const Dev& D, uint32_t budget, hipStream_t s);
 hipError_t launch_reset(const Dev& D, hipStream_t s);
 hipError_t launch_reduce(const Dev& D, unsigned long long* out, uint64_t cluster_base,
@@ -58,7 +57,6 @@ struct mr_batch {
   Dev D;
   void* base = nullptr;
   size_t bytes = 0;
-  uint64_t* prog = nullptr;
   unsigned long long* red = nullptr;
   uint32_t* h_remaining = nullptr;
   hipStream_t stream = nullptr;
@@ -162,9 +160,11 @@ int mr_batch_create(const mr_cfg* cfg, mr_batch** out) {
   if (!out) return set_err("null out");
   *out = nullptr;
   if (validate(cfg) != 0) return -1;
-  std::vector<uint64_t> prog;
-  if (!build_program(*cfg, prog))
-    return set_err(std::string("scenario has no GPU program yet: ") + k_names[cfg->scenario]);
+  const uint32_t scn = cfg->scenario;
+  if (scn == MR_SCN_UNRELIABLE_AGREE_2C || scn == MR_SCN_RELIABLE_CHURN_2C ||
+      scn == MR_SCN_UNRELIABLE_CHURN_2C)
+    return set_err(std::string("scenario needs concurrent tester tasks (not built yet): ") +
+                   k_names[scn]);
 
   mr_batch* b = new mr_batch();
   b->cfg = *cfg;
@@ -178,7 +178,11 @@ int mr_batch_create(const mr_cfg* cfg, mr_batch** out) {
   D.unrel_flag = (cfg->flags & MR_F_UNRELIABLE) ? 1u : 0u;
   D.trace_clusters = (cfg->flags & MR_F_TRACE) ? cfg->trace_clusters : 0u;
   D.trace_cap = cfg->trace_cap;
-  D.prog_len = (uint32_t)prog.size();
+  D.scenario = scn;
+  // loop counts of the test bodies (tests.rs): many_election 10, figure_8 1000, snap_common 30
+  uint32_t def_iters = scn == MR_SCN_MANY_ELECTION_2A ? 10 : (scn >= MR_SCN_SNAPSHOT_BASIC_2D &&
+                       scn <= MR_SCN_SNAPSHOT_INSTALL_UNRELIABLE_CRASH_2D) ? 30 : 1000;
+  D.iters = cfg->iters ? cfg->iters : def_iters;
   D.seed0 = cfg->seed_base + cfg->cluster_base;
 
   // carve one allocation; every array 256-B aligned
@@ -187,31 +191,26 @@ int mr_batch_create(const mr_cfg* cfg, mr_batch** out) {
   auto add = [&](auto** p, size_t count) {
     items.push_back({reinterpret_cast<void**>(p), count * sizeof(**p)});
   };
-  add(&D.code, C);
-  for (uint32_t** p : {&D.vtime, &D.now, &D.events, &D.msgs_sent, &D.inflight, &D.netmode,
-                       &D.t_ctr, &D.trace_n, &D.mslot})
-    add(p, C);
-  for (uint64_t** p : {&D.free_mask, &D.digest, &D.mmin}) add(p, C);
-  add(&D.cnt, (size_t)CNT__N * C);
-  for (uint32_t** p : {&D.nflags, &D.nterm, &D.ncommit, &D.napplied, &D.nlast, &D.nsnap,
-                       &D.nsnapt, &D.ntimer, &D.nectr, &D.nnctr, &D.slen})
-    add(p, n * C);
+  // field matrices use 32-bit element offsets in the kernels
+  const uint64_t lim = 1ull << 32;
+  if ((uint64_t)CS__N * C >= lim || (uint64_t)C64__N * C >= lim || NF__N * n * C >= lim ||
+      PF__N * n * n * C >= lim || MF__N * M * C >= lim || M64__N * M * C >= lim) {
+    delete b;
+    return set_err("n_clusters too large for one batch (32-bit field offsets)");
+  }
+  add(&D.cs32, (size_t)CS__N * C);
+  add(&D.cs64, (size_t)C64__N * C);
+  add(&D.nd32, (size_t)NF__N * n * C);
   add(&D.nsnapv, n * C);
-  add(&D.nnext, n * n * C);
-  add(&D.nmatch, n * n * C);
+  add(&D.pr32, (size_t)PF__N * n * n * C);
+  add(&D.ms32, (size_t)MF__N * M * C);
+  add(&D.ms64, (size_t)M64__N * M * C);
   add(&D.lterm, C * n * cfg->log_cap);
   add(&D.lval, C * n * cfg->log_cap);
-  add(&D.mkey, M * C);
-  for (uint32_t** p : {&D.mhdr, &D.mterm, &D.ma, &D.mb, &D.mc}) add(p, M * C);
-  add(&D.mv, M * C);
   add(&D.pterm, C * M * K);
   add(&D.pval, C * M * K);
   add(&D.smask, C * cfg->apply_cap);
   add(&D.sval, C * cfg->apply_cap);
-  for (uint32_t** p : {&D.tpc, &D.twake, &D.tphase}) add(p, C);
-  add(&D.ts, (size_t)N_S * C);
-  add(&D.tr, (size_t)N_R * C);
-  add(&D.tv, (size_t)N_V * C);
   add(&D.trace, (size_t)D.trace_clusters * D.trace_cap);
   add(&D.remaining, 1);
   size_t total = 0;
@@ -219,14 +218,11 @@ int mr_batch_create(const mr_cfg* cfg, mr_batch** out) {
 
   hipError_t e = hipSetDevice(cfg->device);
   if (e == hipSuccess) e = hipMalloc(&b->base, total);
-  if (e == hipSuccess) e = hipMalloc(&b->prog, prog.size() * sizeof(uint64_t));
   if (e == hipSuccess) e = hipMalloc(&b->red, RED_N * sizeof(unsigned long long));
   if (e == hipSuccess) e = hipHostMalloc(&b->h_remaining, sizeof(uint32_t));
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&b->stream, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipEventCreate(&b->ev0);
   if (e == hipSuccess) e = hipEventCreate(&b->ev1);
-  if (e == hipSuccess)
-    e = hipMemcpy(b->prog, prog.data(), prog.size() * sizeof(uint64_t), hipMemcpyHostToDevice);
   if (e != hipSuccess) {
     std::string msg = std::string("allocation of ") + std::to_string(total) + " B failed: " +
                       hipGetErrorString(e);
@@ -239,7 +235,6 @@ int mr_batch_create(const mr_cfg* cfg, mr_batch** out) {
     *it.p = p;
     p += (it.bytes + 255) & ~size_t(255);
   }
-  D.prog = b->prog;
   if (const char* s = std::getenv("MR_STEP_BUDGET")) b->budget = (uint32_t)std::atoi(s);
   if (b->budget == 0) b->budget = 2048;
   if (mr_batch_reset(b, cfg->seed_base) != 0) {
@@ -304,10 +299,20 @@ int mr_batch_verdicts(mr_batch* b, uint16_t* code, uint32_t* time_us, uint64_t* 
   if (!b) return set_err("null batch");
   HIPCHK(hipSetDevice(b->cfg.device));
   size_t C = b->D.C;
-  if (code) HIPCHK(hipMemcpyAsync(code, b->D.code, C * 2, hipMemcpyDeviceToHost, b->stream));
-  if (time_us) HIPCHK(hipMemcpyAsync(time_us, b->D.vtime, C * 4, hipMemcpyDeviceToHost, b->stream));
-  if (digest) HIPCHK(hipMemcpyAsync(digest, b->D.digest, C * 8, hipMemcpyDeviceToHost, b->stream));
+  std::vector<uint32_t> c32;
+  if (code) {
+    c32.resize(C);
+    HIPCHK(hipMemcpyAsync(c32.data(), b->D.cs32 + (size_t)CS_CODE * C, C * 4,
+                          hipMemcpyDeviceToHost, b->stream));
+  }
+  if (time_us)
+    HIPCHK(hipMemcpyAsync(time_us, b->D.cs32 + (size_t)CS_VTIME * C, C * 4, hipMemcpyDeviceToHost,
+                          b->stream));
+  if (digest)
+    HIPCHK(hipMemcpyAsync(digest, b->D.cs64 + (size_t)C64_DIGEST * C, C * 8,
+                          hipMemcpyDeviceToHost, b->stream));
   HIPCHK(hipStreamSynchronize(b->stream));
+  for (size_t i = 0; i < c32.size(); i++) code[i] = (uint16_t)c32[i];
   return 0;
 }
 
@@ -336,9 +341,9 @@ int mr_batch_counters(mr_batch* b, mr_counters* out) {
   for (int i = 0; i < 64; i++) out->fail_hist[i] = h[CNT__N + 8 + i];
   out->first_fail_code = 0;
   if (out->first_fail_cluster != ~0ull) {
-    uint16_t code = 0;
+    uint32_t code = 0;
     size_t idx = out->first_fail_cluster - b->cfg.cluster_base;
-    HIPCHK(hipMemcpy(&code, b->D.code + idx, 2, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(&code, b->D.cs32 + (size_t)CS_CODE * b->D.C + idx, 4, hipMemcpyDeviceToHost));
     out->first_fail_code = code;
   }
   return 0;
@@ -349,7 +354,7 @@ int mr_trace_get(mr_batch* b, uint32_t k, mr_event* out, size_t cap, size_t* n) 
   if (k >= b->D.trace_clusters) return set_err("cluster not traced");
   HIPCHK(hipSetDevice(b->cfg.device));
   uint32_t tn = 0;
-  HIPCHK(hipMemcpy(&tn, b->D.trace_n + k, 4, hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(&tn, b->D.cs32 + (size_t)CS_TRACEN * b->D.C + k, 4, hipMemcpyDeviceToHost));
   size_t m = tn < b->D.trace_cap ? tn : b->D.trace_cap;
   if (m > cap) m = cap;
   HIPCHK(hipMemcpy(out, b->D.trace + (size_t)k * b->D.trace_cap, m * sizeof(mr_event),
@@ -363,7 +368,6 @@ void mr_batch_destroy(mr_batch* b) {
   (void)hipSetDevice(b->cfg.device);
   if (b->stream) (void)hipStreamSynchronize(b->stream);
   if (b->base) (void)hipFree(b->base);
-  if (b->prog) (void)hipFree(b->prog);
   if (b->red) (void)hipFree(b->red);
   if (b->h_remaining) (void)hipHostFree(b->h_remaining);
   if (b->ev0) (void)hipEventDestroy(b->ev0);

@@ -17,7 +17,7 @@ from . import _abi
 from ._abi import EVENT_DTYPE, FAIL_NAMES, MrCfg, MrCounters, MrRunStats
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libmadraft_hip.so")
+LIB_PATH = os.environ.get("MADRAFT_HIP_LIB") or os.path.join(_HERE, "lib", "libmadraft_hip.so")
 _lib = None
 
 
