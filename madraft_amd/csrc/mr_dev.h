@@ -17,8 +17,8 @@
 
 namespace mr {
 
-// ---- node flag word (one u32 per node): role[0:2) alive[2] conn[3]
-//      voted[4:8) (15 = none) inc[8:16) votes[16:24)
+// ---- node flag word (one u32 per node): role[0:2) voted[4:8) (15 = none)
+//      inc[8:16) votes[16:24); started / connected are cluster bit masks (CS_ALIVE, CS_CONN)
 enum : uint32_t { R_F = 0, R_C = 1, R_L = 2, R_DOWN = 3 };
 enum : uint32_t { M_RV_REQ = 1, M_RV_REP, M_AE_REQ, M_AE_REP, M_IS_REQ, M_IS_REP };
 enum : uint32_t { ST_TESTER = 1, ST_ELECT = 2, ST_NET = 3 };
@@ -39,7 +39,7 @@ constexpr uint32_t T_NV = 16;  // u64 script arrays (count_2b / concurrent_start
 // cs32 [CS__N][C]: per-cluster u32 scalars
 enum : uint32_t {
   CS_CODE, CS_VTIME, CS_NOW, CS_EVENTS, CS_MSGS, CS_INFLIGHT, CS_NETMODE, CS_TCTR, CS_TRACEN,
-  CS_MSLOT, CS_TPC, CS_TWAKE, CS_TRES, CS_TL, CS_TH = CS_TL + T_NL, CS_CNT = CS_TH + T_NH,
+  CS_MSLOT, CS_CONN, CS_ALIVE, CS_TPC, CS_TWAKE, CS_TRES, CS_TL, CS_TH = CS_TL + T_NL, CS_CNT = CS_TH + T_NH,
   CS__N = CS_CNT + CNT__N
 };
 // cs64 [C64__N][C]: per-cluster u64 scalars

@@ -37,7 +37,9 @@ constexpr uint32_t ELECTION_US = 1000000;  // RAFT_ELECTION_TIMEOUT, tests.rs:18
 struct X {
   uint32_t c, now, events, msgs_sent, inflight, code, trace_n, mslot, netmode, t_ctr;
   uint32_t sleep_us, yield;
+  uint32_t conn, alive;  // node bit masks: connected (net clog state), started (tester.rs:24-25)
   uint64_t free_mask, digest, mmin;
+  uint32_t timer[MR_MAX_NODES];  // node timers (election / heartbeat deadline), INF_T = none
   uint32_t cnt[CNT__N];
 };
 
@@ -51,9 +53,8 @@ struct X {
 #define MS64(f, mi) D.ms64[(uint32_t)(f) * D.M * D.C + (mi)]
 
 // ---------------------------------------------------------------- helpers
+// node flag word: role[0:2) voted[4:8) (15 = none) inc[8:16) votes[16:24)
 DI uint32_t f_role(uint32_t f) { return f & 3u; }
-DI uint32_t f_alive(uint32_t f) { return (f >> 2) & 1u; }
-DI uint32_t f_conn(uint32_t f) { return (f >> 3) & 1u; }
 DI uint32_t f_voted(uint32_t f) { return (f >> 4) & 15u; }
 DI uint32_t f_inc(uint32_t f) { return (f >> 8) & 255u; }
 DI uint32_t f_votes(uint32_t f) { return (f >> 16) & 255u; }
@@ -61,15 +62,28 @@ DI uint32_t f_set(uint32_t f, uint32_t sh, uint32_t w, uint32_t v) {
   uint32_t m = ((1u << w) - 1u) << sh;
   return (f & ~m) | ((v << sh) & m);
 }
+DI uint32_t bit(uint32_t m, uint32_t i) { return (m >> i) & 1u; }
 DI uint32_t u_range(uint32_t w, uint32_t lo, uint32_t hi) {
   return lo + (uint32_t)(((uint64_t)w * (uint64_t)(hi - lo)) >> 32);
 }
+// timers live in registers; a node index is per-lane, so reads / writes are
+// unrolled selects instead of dynamic register indexing
+DI uint32_t get_timer(const X& x, uint32_t d) {
+  uint32_t v = x.timer[0];
+#pragma unroll
+  for (uint32_t j = 1; j < MR_MAX_NODES; j++) v = (d == j) ? x.timer[j] : v;
+  return v;
+}
+DI void set_timer(X& x, uint32_t d, uint32_t t) {
+#pragma unroll
+  for (uint32_t j = 0; j < MR_MAX_NODES; j++) x.timer[j] = (d == j) ? t : x.timer[j];
+}
 
-// Philox4x32-10, counter (c0, c1, c2, 0), key = the cluster's seed; returns w0, w1
-DI void philox(const Dev& D, const X& x, uint32_t c0, uint32_t c1, uint32_t c2, uint32_t& w0,
-               uint32_t& w1) {
-  uint64_t seed = D.seed0 + x.c;
-  uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32), c3 = 0;
+// Philox4x32-10 with counter (c0, c1, c2, 0) and key (k0, k1); returns (w0, w1).
+// Out of line: one copy serves every draw site of the kernel.
+__device__ __forceinline__ uint2 philox2(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t k0,
+                                      uint32_t k1) {
+  uint32_t c3 = 0;
 #pragma unroll
   for (int r = 0; r < 10; r++) {
     uint32_t hi0 = __umulhi(0xD2511F53u, c0), lo0 = 0xD2511F53u * c0;
@@ -78,16 +92,40 @@ DI void philox(const Dev& D, const X& x, uint32_t c0, uint32_t c1, uint32_t c2, 
     c0 = n0; c1 = lo1; c2 = n2; c3 = lo0;
     k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
   }
-  w0 = c0; w1 = c1;
+  return make_uint2(c0, c1);
 }
-
+// the cluster's draw: key = its seed (SEMANTICS ยง2)
+DI void philox(const Dev& D, const X& x, uint32_t c0, uint32_t c1, uint32_t c2, uint32_t& w0,
+               uint32_t& w1) {
+  uint64_t seed = D.seed0 + x.c;
+  uint2 w = philox2(c0, c1, c2, (uint32_t)seed, (uint32_t)(seed >> 32));
+  w0 = w.x;
+  w1 = w.y;
+}
 DI size_t logi(const Dev& D, const X& x, uint32_t d, uint32_t i) {
   return ((size_t)x.c * D.n + d) * D.log_cap + (i & (D.log_cap - 1u));
 }
-DI uint32_t term_at(const Dev& D, const X& x, uint32_t d, uint32_t i, uint32_t snap,
-                    uint32_t snapt) {
+
+// One node's scalar state, loaded into registers at the start of an event
+// (one batch of independent loads) and stored back at its end.
+struct NC {
+  uint32_t f, term, commit, applied, last, snap, snapt, ectr, nctr;
+};
+DI NC load_node(const Dev& D, const X& x, uint32_t d) {
+  NC n;
+  n.f = ND(NF_FLAGS, d); n.term = ND(NF_TERM, d); n.commit = ND(NF_COMMIT, d);
+  n.applied = ND(NF_APPLIED, d); n.last = ND(NF_LAST, d); n.snap = ND(NF_SNAP, d);
+  n.snapt = ND(NF_SNAPT, d); n.ectr = ND(NF_ECTR, d); n.nctr = ND(NF_NCTR, d);
+  return n;
+}
+DI void store_node(const Dev& D, const X& x, uint32_t d, const NC& n) {
+  ND(NF_FLAGS, d) = n.f; ND(NF_TERM, d) = n.term; ND(NF_COMMIT, d) = n.commit;
+  ND(NF_APPLIED, d) = n.applied; ND(NF_LAST, d) = n.last; ND(NF_SNAP, d) = n.snap;
+  ND(NF_SNAPT, d) = n.snapt; ND(NF_ECTR, d) = n.ectr; ND(NF_NCTR, d) = n.nctr;
+}
+DI uint32_t term_at(const Dev& D, const X& x, uint32_t d, const NC& n, uint32_t i) {
   if (i == 0) return 0;
-  if (i == snap) return snapt;
+  if (i == n.snap) return n.snapt;
   return D.lterm[logi(D, x, d, i)];
 }
 
@@ -95,12 +133,17 @@ DI uint32_t net_loss(const X& x) { return (x.netmode & 1u) ? LOSS_Q32 : 0u; }  /
 DI uint32_t net_lat_hi(const X& x) { return (x.netmode & 1u) ? 27000u : 10000u; }
 
 // ---------------------------------------------------------------- trace
-DI void rec8(const Dev& D, X& x, uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3, uint32_t w4,
-             uint32_t w5, uint32_t w6, uint32_t w7) {
-  uint64_t h = x.digest;
+// FNV-1a-64 over the 8 words of one trace record (out of line: one copy)
+__device__ __forceinline__ uint64_t fnv8(uint64_t h, uint32_t w0, uint32_t w1, uint32_t w2,
+                                      uint32_t w3, uint32_t w4, uint32_t w5, uint32_t w6,
+                                      uint32_t w7) {
   h = (h ^ w0) * FNV_P; h = (h ^ w1) * FNV_P; h = (h ^ w2) * FNV_P; h = (h ^ w3) * FNV_P;
   h = (h ^ w4) * FNV_P; h = (h ^ w5) * FNV_P; h = (h ^ w6) * FNV_P; h = (h ^ w7) * FNV_P;
-  x.digest = h;
+  return h;
+}
+DI void rec8(const Dev& D, X& x, uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3, uint32_t w4,
+             uint32_t w5, uint32_t w6, uint32_t w7) {
+  x.digest = fnv8(x.digest, w0, w1, w2, w3, w4, w5, w6, w7);
   if (x.c < D.trace_clusters && x.trace_n < D.trace_cap) {
     uint32_t* p = reinterpret_cast<uint32_t*>(D.trace + (size_t)x.c * D.trace_cap + x.trace_n);
     p[0] = w0; p[1] = w1; p[2] = w2; p[3] = w3; p[4] = w4; p[5] = w5; p[6] = w6; p[7] = w7;
@@ -108,11 +151,11 @@ DI void rec8(const Dev& D, X& x, uint32_t w0, uint32_t w1, uint32_t w2, uint32_t
   x.trace_n++;
 }
 
-DI void rec_node(const Dev& D, X& x, uint32_t cls, uint32_t kind, uint32_t d, uint32_t aux) {
-  uint32_t f = ND(NF_FLAGS, d);
-  uint32_t role = f_alive(f) ? f_role(f) : R_DOWN;
-  rec8(D, x, x.now, cls | (kind << 8) | (d << 16) | (role << 24), aux, ND(NF_TERM, d),
-       ND(NF_COMMIT, d), ND(NF_APPLIED, d), ND(NF_LAST, d), ND(NF_SNAP, d));
+DI void rec_node(const Dev& D, X& x, uint32_t cls, uint32_t kind, uint32_t d, uint32_t aux,
+                 const NC& n) {
+  uint32_t role = bit(x.alive, d) ? f_role(n.f) : R_DOWN;
+  rec8(D, x, x.now, cls | (kind << 8) | (d << 16) | (role << 24), aux, n.term, n.commit,
+       n.applied, n.last, n.snap);
 }
 
 DI void rec_simple(const Dev& D, X& x, uint32_t cls, uint32_t kind) {
@@ -126,12 +169,10 @@ DI void fail(const Dev& D, X& x, uint32_t code) {
 }
 
 // ---------------------------------------------------------------- timers / net
-DI void reset_timer(const Dev& D, X& x, uint32_t d) {  // raft.rs:260-263
-  uint32_t ctr = ND(NF_ECTR, d);
-  ND(NF_ECTR, d) = ctr + 1;
+DI void reset_timer(const Dev& D, X& x, uint32_t d, NC& n) {  // raft.rs:260-263
   uint32_t w0, w1;
-  philox(D, x, ctr, d, ST_ELECT, w0, w1);
-  ND(NF_TIMER, d) = x.now + u_range(w0, D.elo, D.ehi);
+  philox(D, x, n.ectr++, d, ST_ELECT, w0, w1);
+  set_timer(x, d, x.now + u_range(w0, D.elo, D.ehi));
 }
 
 DI void rescan_min(const Dev& D, X& x) {
@@ -147,13 +188,14 @@ DI void rescan_min(const Dev& D, X& x) {
   x.mslot = bs;
 }
 
-// madsim net send (tester.rs:127-137, :147-149). Returns the slot or -1.
-DI int net_send(const Dev& D, X& x, uint32_t src, uint32_t dst, uint32_t type, uint32_t inc,
-                uint32_t term, uint32_t a, uint32_t b, uint32_t c, uint64_t v, uint32_t k) {
+// madsim net send from node `src` (whose state is `s`) (tester.rs:127-137,
+// :147-149). Returns the slot or -1 if the message is dropped.
+DI int net_send(const Dev& D, X& x, uint32_t src, NC& s, uint32_t dst, uint32_t type,
+                uint32_t inc, uint32_t term, uint32_t a, uint32_t b, uint32_t c, uint64_t v,
+                uint32_t k) {
   uint32_t seq = x.msgs_sent++;
-  uint32_t ctr = ND(NF_NCTR, src);
-  ND(NF_NCTR, src) = ctr + 1;
-  if (!f_conn(ND(NF_FLAGS, src)) || !f_conn(ND(NF_FLAGS, dst))) { x.cnt[CNT_DROP_CLOG]++; return -1; }
+  uint32_t ctr = s.nctr++;
+  if (!bit(x.conn, src) || !bit(x.conn, dst)) { x.cnt[CNT_DROP_CLOG]++; return -1; }
   uint32_t w0, w1;
   philox(D, x, ctr, src, ST_NET, w0, w1);
   if (w0 < net_loss(x)) { x.cnt[CNT_DROP_LOSS]++; return -1; }
@@ -166,7 +208,8 @@ DI int net_send(const Dev& D, X& x, uint32_t src, uint32_t dst, uint32_t type, u
   uint32_t mi = slot * D.C + x.c;
   MS64(M64_KEY, mi) = key;
   MS32(MF_HDR, mi) = type | (src << 3) | (dst << 6) | (inc << 9) | (k << 17);
-  MS32(MF_TERM, mi) = term; MS32(MF_A, mi) = a; MS32(MF_B, mi) = b; MS32(MF_C, mi) = c; MS64(M64_V, mi) = v;
+  MS32(MF_TERM, mi) = term; MS32(MF_A, mi) = a; MS32(MF_B, mi) = b; MS32(MF_C, mi) = c;
+  if (type == M_IS_REQ) MS64(M64_V, mi) = v;
   x.inflight++;
   if (x.inflight > x.cnt[CNT_MAX_INFLIGHT]) x.cnt[CNT_MAX_INFLIGHT] = x.inflight;
   if (key < x.mmin) { x.mmin = key; x.mslot = slot; }
@@ -208,249 +251,247 @@ DI uint32_t n_committed(const Dev& D, X& x, uint32_t idx, uint64_t& v) {  // tes
 }
 
 // ---------------------------------------------------------------- Raft node
-DI void node_apply(const Dev& D, X& x, uint32_t me) {  // tester.rs:302-325 applier
-  uint32_t applied = ND(NF_APPLIED, me), commit = ND(NF_COMMIT, me);
-  uint32_t snap = ND(NF_SNAP, me), snapt = ND(NF_SNAPT, me);
+// One node event (a message delivery or a timer firing) runs in four phases
+// so that the kernel holds exactly one copy of the send path:
+//   decode + load the node's state into registers -> handler (state changes
+//   only; it names the messages to send) -> apply newly committed entries
+//   (the tester's applier) -> send loop over the named peers, ascending ->
+//   store the node, append the trace record.
+// The order of observable effects is the same as calling send() inline in the
+// handlers (SEMANTICS ยง5): every send of an event happens after its state
+// changes and its applies, in ascending peer order.
+enum : uint32_t { SEND_NONE = 0, SEND_REPLY, SEND_APPEND, SEND_VOTE };
+
+DI void node_apply(const Dev& D, X& x, uint32_t me, NC& d) {  // tester.rs:302-325 applier
   bool snapmode = (x.netmode >> 1) & 1u;
-  while (applied < commit) {
-    applied++;
-    uint64_t v = D.lval[logi(D, x, me, applied)];
-    push_and_check(D, x, me, applied, v);
+  while (d.applied < d.commit) {
+    uint32_t i = ++d.applied;
+    uint64_t v = D.lval[logi(D, x, me, i)];
+    push_and_check(D, x, me, i, v);
     if (x.code != RUN) return;
-    if (snapmode && (applied + 1) % 10u == 0 && applied > snap) {
-      snapt = term_at(D, x, me, applied, snap, snapt);
-      snap = applied;
-      ND(NF_SNAP, me) = snap; ND(NF_SNAPT, me) = snapt; NSV(me) = v;
+    if (snapmode && (i + 1) % 10u == 0 && i > d.snap) {
+      d.snapt = term_at(D, x, me, d, i);
+      d.snap = i;
+      NSV(me) = v;
       x.cnt[CNT_SNAPSHOTS]++;
     }
   }
-  ND(NF_APPLIED, me) = applied;
-}
-
-DI void send_append(const Dev& D, X& x, uint32_t l, uint32_t p) {
-  uint32_t nx = PR(PF_NEXT, l, p), snap = ND(NF_SNAP, l), snapt = ND(NF_SNAPT, l), term = ND(NF_TERM, l);
-  uint32_t inc = f_inc(ND(NF_FLAGS, l));
-  if (nx <= snap) {
-    net_send(D, x, l, p, M_IS_REQ, inc, term, snap, snapt, 0, NSV(l), 0);
-    return;
-  }
-  uint32_t prev = nx - 1, last = ND(NF_LAST, l);
-  uint32_t k = last - prev;
-  if (k > D.K) k = D.K;
-  uint32_t pt = term_at(D, x, l, prev, snap, snapt);
-  x.cnt[CNT_SHIPPED] += k;
-  int slot = net_send(D, x, l, p, M_AE_REQ, inc, term, prev, pt, ND(NF_COMMIT, l), 0, k);
-  if (slot >= 0) {
-    size_t pb = ((size_t)x.c * D.M + (uint32_t)slot) * D.K;
-    for (uint32_t j = 0; j < k; j++) {
-      size_t li = logi(D, x, l, prev + 1 + j);
-      D.pterm[pb + j] = D.lterm[li];
-      D.pval[pb + j] = D.lval[li];
-    }
-  }
-}
-
-DI void become_leader(const Dev& D, X& x, uint32_t me) {
-  ND(NF_FLAGS, me) = f_set(ND(NF_FLAGS, me), 0, 2, R_L);
-  x.cnt[CNT_LEADERS]++;
-  uint32_t last = ND(NF_LAST, me);
-  for (uint32_t p = 0; p < D.n; p++) { PR(PF_NEXT, me, p) = last + 1; PR(PF_MATCH, me, p) = 0; }
-  PR(PF_MATCH, me, me) = last;
-  for (uint32_t p = 0; p < D.n; p++) {
-    if (p == me) continue;
-    send_append(D, x, me, p);
-    if (x.code != RUN) return;
-  }
-  ND(NF_TIMER, me) = x.now + D.hb;
 }
 
 // commit = the majority-th largest match index, if it is from the current term
-DI void advance_commit(const Dev& D, X& x, uint32_t me) {
-  uint32_t last = ND(NF_LAST, me), maj = D.n / 2 + 1, N = 0;
-  for (uint32_t i = 0; i < D.n; i++) {
-    uint32_t mi = (i == me) ? last : PR(PF_MATCH, me, i);
-    if (mi <= N) continue;
+DI void advance_commit(const Dev& D, X& x, uint32_t me, NC& d) {
+  uint32_t mv[MR_MAX_NODES];
+#pragma unroll
+  for (uint32_t p = 0; p < MR_MAX_NODES; p++)
+    mv[p] = (p < D.n) ? ((p == me) ? d.last : PR(PF_MATCH, me, p)) : 0u;
+  uint32_t maj = D.n / 2 + 1, N = 0;
+#pragma unroll
+  for (uint32_t i = 0; i < MR_MAX_NODES; i++) {
     uint32_t ge = 0;
-    for (uint32_t j = 0; j < D.n; j++) {
-      uint32_t mj = (j == me) ? last : PR(PF_MATCH, me, j);
-      ge += (mj >= mi) ? 1u : 0u;
+#pragma unroll
+    for (uint32_t j = 0; j < MR_MAX_NODES; j++) ge += (j < D.n && mv[j] >= mv[i]) ? 1u : 0u;
+    if (i < D.n && ge >= maj && mv[i] > N) N = mv[i];
+  }
+  if (N > d.commit && term_at(D, x, me, d, N) == d.term) d.commit = N;
+}
+
+// AppendEntries / InstallSnapshot acknowledgement up to xv; returns the peer
+// mask to send a follow-up append to
+DI uint32_t on_ack(const Dev& D, X& x, uint32_t me, NC& d, uint32_t p, uint32_t xv) {
+  uint32_t m = PR(PF_MATCH, me, p), nx = PR(PF_NEXT, me, p);
+  if (xv > m) PR(PF_MATCH, me, p) = xv;
+  if (xv + 1 > nx) { nx = xv + 1; PR(PF_NEXT, me, p) = nx; }
+  advance_commit(D, x, me, d);
+  return nx <= d.last ? (1u << p) : 0u;  // still behind: pipeline the next batch
+}
+
+DI void node_event(const Dev& D, X& x, bool is_msg, uint32_t tnode, uint32_t slot,
+                   uint32_t seq) {
+  uint32_t me = tnode, src = 0, type = 0, inc = 0, k = 0, mterm = 0, ma = 0, mb = 0, mc = 0;
+  uint32_t mi = 0;
+  if (is_msg) {
+    mi = slot * D.C + x.c;
+    uint32_t hdr = MS32(MF_HDR, mi);
+    mterm = MS32(MF_TERM, mi); ma = MS32(MF_A, mi); mb = MS32(MF_B, mi); mc = MS32(MF_C, mi);
+    type = hdr & 7u; src = (hdr >> 3) & 7u; me = (hdr >> 6) & 7u; inc = (hdr >> 9) & 255u;
+    k = (hdr >> 17) & 63u;
+    MS64(M64_KEY, mi) = ~0ull;
+    x.free_mask |= 1ull << slot;
+    x.inflight--;
+    rescan_min(D, x);
+  }
+  NC d = load_node(D, x, me);
+  uint32_t mode = SEND_NONE, peers = 0, rtype = 0, ra = 0, rb = 0, kind;
+  const uint32_t others = ((1u << D.n) - 1u) & ~(1u << me);
+  if (is_msg) {
+    kind = type;
+    if (!bit(x.alive, me) || !bit(x.conn, me) || !bit(x.conn, src)) {
+      x.cnt[CNT_DROP_DELIVER]++;
+      rec_node(D, x, 0, 16, me, seq, d);
+      return;
     }
-    if (ge >= maj) N = mi;
-  }
-  if (N > ND(NF_COMMIT, me) &&
-      term_at(D, x, me, N, ND(NF_SNAP, me), ND(NF_SNAPT, me)) == ND(NF_TERM, me)) {
-    ND(NF_COMMIT, me) = N;
-    node_apply(D, x, me);
-  }
-}
-
-DI void on_ack(const Dev& D, X& x, uint32_t me, uint32_t p, uint32_t xv) {
-  if (xv > PR(PF_MATCH, me, p)) PR(PF_MATCH, me, p) = xv;
-  if (xv + 1 > PR(PF_NEXT, me, p)) PR(PF_NEXT, me, p) = xv + 1;
-  advance_commit(D, x, me);
-  if (x.code != RUN) return;
-  if (PR(PF_NEXT, me, p) <= ND(NF_LAST, me)) send_append(D, x, me, p);
-}
-
-DI void deliver(const Dev& D, X& x, uint32_t slot, uint32_t seq) {
-  uint32_t mi = slot * D.C + x.c;
-  uint32_t hdr = MS32(MF_HDR, mi);
-  uint32_t type = hdr & 7u, src = (hdr >> 3) & 7u, me = (hdr >> 6) & 7u, inc = (hdr >> 9) & 255u;
-  uint32_t k = (hdr >> 17) & 63u;
-  uint32_t mterm = MS32(MF_TERM, mi), ma = MS32(MF_A, mi), mb = MS32(MF_B, mi), mc = MS32(MF_C, mi);
-  uint64_t mv = MS64(M64_V, mi);
-  MS64(M64_KEY, mi) = ~0ull;
-  x.free_mask |= 1ull << slot;
-  x.inflight--;
-  rescan_min(D, x);
-
-  uint32_t f = ND(NF_FLAGS, me);
-  if (!f_alive(f) || !f_conn(f) || !f_conn(ND(NF_FLAGS, src))) {
-    x.cnt[CNT_DROP_DELIVER]++;
-    rec_node(D, x, 0, 16, me, seq);
-    return;
-  }
-  bool is_reply = (type == M_RV_REP || type == M_AE_REP || type == M_IS_REP);
-  if (is_reply && inc != f_inc(f)) {
-    x.cnt[CNT_DROP_STALE]++;
-    rec_node(D, x, 0, 17, me, seq);
-    return;
-  }
-  uint32_t term = ND(NF_TERM, me);
-  if (mterm > term) {  // step down
-    uint32_t was = f_role(f);
-    term = mterm;
-    ND(NF_TERM, me) = term;
-    f = f_set(f_set(f_set(f, 4, 4, 15u), 16, 8, 0u), 0, 2, R_F);
-    ND(NF_FLAGS, me) = f;
-    if (was == R_L) reset_timer(D, x, me);
-  }
-  uint32_t role = f_role(f);
-  switch (type) {
-    case M_RV_REQ: {
-      uint32_t last = ND(NF_LAST, me);
-      uint32_t lt = term_at(D, x, me, last, ND(NF_SNAP, me), ND(NF_SNAPT, me));
-      bool up = (mc > lt) || (mc == lt && mb >= last);
-      uint32_t voted = f_voted(f);
-      bool granted = (mterm == term) && (voted == 15u || voted == ma) && up;
-      if (granted) {
-        ND(NF_FLAGS, me) = f_set(f, 4, 4, ma);
-        reset_timer(D, x, me);
-      }
-      net_send(D, x, me, src, M_RV_REP, inc, term, granted ? 1u : 0u, 0, 0, 0, 0);
-    } break;
-    case M_RV_REP:
-      if (role == R_C && mterm == term && ma) {
-        uint32_t votes = f_votes(f) | (1u << src);
-        ND(NF_FLAGS, me) = f_set(f, 16, 8, votes);
-        if ((uint32_t)__builtin_popcount(votes) > D.n / 2) become_leader(D, x, me);
-      }
-      break;
-    case M_AE_REQ: {
-      if (mterm < term) { net_send(D, x, me, src, M_AE_REP, inc, term, 0, 0, 0, 0, 0); break; }
-      if (role == R_C) ND(NF_FLAGS, me) = f_set(f, 0, 2, R_F);
-      reset_timer(D, x, me);
-      uint32_t snap = ND(NF_SNAP, me), snapt = ND(NF_SNAPT, me), last = ND(NF_LAST, me);
-      uint32_t prev = ma, pterm = mb, j0 = 0;
-      if (prev < snap) {
-        uint32_t skip = snap - prev;
-        j0 = skip < k ? skip : k;
-        prev = snap; pterm = snapt;
-      }
-      if (prev > last) {
-        net_send(D, x, me, src, M_AE_REP, inc, term, 0, last + 1, 0, 0, 0);
-        break;
-      }
-      uint32_t tp = term_at(D, x, me, prev, snap, snapt);
-      if (tp != pterm) {
-        uint32_t xx = prev;
-        while (xx - 1 > snap && term_at(D, x, me, xx - 1, snap, snapt) == tp) xx--;
-        net_send(D, x, me, src, M_AE_REP, inc, term, 0, xx, 0, 0, 0);
-        break;
-      }
-      size_t pb = ((size_t)x.c * D.M + slot) * D.K;
-      for (uint32_t j = j0; j < k; j++) {
-        uint32_t i = ma + 1 + j, et = D.pterm[pb + j];
-        if (i <= last && term_at(D, x, me, i, snap, snapt) == et) continue;
-        if (i - snap > D.log_cap) { fail(D, x, MR_FAIL_SIM_CAPACITY); return; }
-        size_t li = logi(D, x, me, i);
-        D.lterm[li] = et;
-        D.lval[li] = D.pval[pb + j];
-        last = i;
-        if (i - snap > x.cnt[CNT_MAX_LOG]) x.cnt[CNT_MAX_LOG] = i - snap;
-      }
-      ND(NF_LAST, me) = last;
-      uint32_t lc = ma + k;
-      if (mc < lc) lc = mc;
-      if (lc > ND(NF_COMMIT, me)) {
-        ND(NF_COMMIT, me) = lc;
-        node_apply(D, x, me);
-        if (x.code != RUN) return;
-      }
-      net_send(D, x, me, src, M_AE_REP, inc, term, 1, ma + k, 0, 0, 0);
-    } break;
-    case M_AE_REP:
-      if (role != R_L || mterm != term) break;
-      if (ma) {
-        on_ack(D, x, me, src, mb);
-      } else {
-        uint32_t xx = mb, lo = PR(PF_MATCH, me, src) + 1, hi = ND(NF_LAST, me) + 1;
-        if (xx < lo) xx = lo;
-        if (xx > hi) xx = hi;
-        PR(PF_NEXT, me, src) = xx;
-        send_append(D, x, me, src);
-      }
-      break;
-    case M_IS_REQ: {
-      if (mterm < term) { net_send(D, x, me, src, M_IS_REP, inc, term, 0, 0, 0, 0, 0); break; }
-      if (role == R_C) ND(NF_FLAGS, me) = f_set(f, 0, 2, R_F);
-      reset_timer(D, x, me);
-      uint32_t idx = ma;
-      if (idx > ND(NF_COMMIT, me)) {
-        uint32_t last = ND(NF_LAST, me);
-        if (!(idx <= last && term_at(D, x, me, idx, ND(NF_SNAP, me), ND(NF_SNAPT, me)) == mb))
-          ND(NF_LAST, me) = idx;
-        ND(NF_SNAP, me) = idx; ND(NF_SNAPT, me) = mb; NSV(me) = mv;
-        ND(NF_COMMIT, me) = idx; ND(NF_APPLIED, me) = idx;
-        storage_snapshot(D, x, me, idx);
-        if (x.code != RUN) return;
-        x.cnt[CNT_INSTALLS]++;
-      }
-      net_send(D, x, me, src, M_IS_REP, inc, term, 0, idx, 0, 0, 0);
-    } break;
-    case M_IS_REP:
-      if (role == R_L && mterm == term && mb > 0) on_ack(D, x, me, src, mb);
-      break;
-  }
-  if (x.code != RUN) return;
-  rec_node(D, x, 0, type, me, seq);
-}
-
-DI void on_timer(const Dev& D, X& x, uint32_t me) {
-  uint32_t f = ND(NF_FLAGS, me);
-  if (f_role(f) == R_L) {  // heartbeat / replication round
-    for (uint32_t p = 0; p < D.n; p++) {
-      if (p == me) continue;
-      send_append(D, x, me, p);
-      if (x.code != RUN) return;
+    bool is_reply = (type == M_RV_REP || type == M_AE_REP || type == M_IS_REP);
+    if (is_reply && inc != f_inc(d.f)) {
+      x.cnt[CNT_DROP_STALE]++;
+      rec_node(D, x, 0, 17, me, seq, d);
+      return;
     }
-    ND(NF_TIMER, me) = x.now + D.hb;
-    rec_node(D, x, 1, 1, me, 0);
-    return;
+    if (mterm > d.term) {  // step down
+      uint32_t was = f_role(d.f);
+      d.term = mterm;
+      d.f = f_set(f_set(f_set(d.f, 4, 4, 15u), 16, 8, 0u), 0, 2, R_F);
+      if (was == R_L) reset_timer(D, x, me, d);
+    }
+    const uint32_t role = f_role(d.f), term = d.term;
+    switch (type) {
+      case M_RV_REQ: {
+        uint32_t lt = term_at(D, x, me, d, d.last);
+        bool up = (mc > lt) || (mc == lt && mb >= d.last);
+        uint32_t voted = f_voted(d.f);
+        bool granted = (mterm == term) && (voted == 15u || voted == ma) && up;
+        if (granted) {
+          d.f = f_set(d.f, 4, 4, ma);
+          reset_timer(D, x, me, d);
+        }
+        mode = SEND_REPLY; rtype = M_RV_REP; ra = granted ? 1u : 0u;
+      } break;
+      case M_RV_REP:
+        if (role == R_C && mterm == term && ma) {
+          uint32_t votes = f_votes(d.f) | (1u << src);
+          d.f = f_set(d.f, 16, 8, votes);
+          if ((uint32_t)__builtin_popcount(votes) > D.n / 2) {  // become leader
+            d.f = f_set(d.f, 0, 2, R_L);
+            x.cnt[CNT_LEADERS]++;
+            for (uint32_t p = 0; p < D.n; p++) {
+              PR(PF_NEXT, me, p) = d.last + 1;
+              PR(PF_MATCH, me, p) = (p == me) ? d.last : 0u;
+            }
+            set_timer(x, me, x.now + D.hb);
+            mode = SEND_APPEND; peers = others;
+          }
+        }
+        break;
+      case M_AE_REQ: {
+        mode = SEND_REPLY; rtype = M_AE_REP;
+        if (mterm < term) break;  // reply {term, false, 0}
+        if (role == R_C) d.f = f_set(d.f, 0, 2, R_F);
+        reset_timer(D, x, me, d);
+        uint32_t prev = ma, pterm = mb, j0 = 0;
+        if (prev < d.snap) {
+          uint32_t skip = d.snap - prev;
+          j0 = skip < k ? skip : k;
+          prev = d.snap; pterm = d.snapt;
+        }
+        if (prev > d.last) { rb = d.last + 1; break; }
+        uint32_t tp = term_at(D, x, me, d, prev);
+        if (tp != pterm) {
+          uint32_t xx = prev;
+          while (xx - 1 > d.snap && term_at(D, x, me, d, xx - 1) == tp) xx--;
+          rb = xx;
+          break;
+        }
+        size_t pb = ((size_t)x.c * D.M + slot) * D.K;
+        for (uint32_t j = j0; j < k; j++) {
+          uint32_t i = ma + 1 + j, et = D.pterm[pb + j];
+          if (i <= d.last && term_at(D, x, me, d, i) == et) continue;
+          if (i - d.snap > D.log_cap) { fail(D, x, MR_FAIL_SIM_CAPACITY); return; }
+          size_t li = logi(D, x, me, i);
+          D.lterm[li] = et;
+          D.lval[li] = D.pval[pb + j];
+          d.last = i;
+          if (i - d.snap > x.cnt[CNT_MAX_LOG]) x.cnt[CNT_MAX_LOG] = i - d.snap;
+        }
+        uint32_t lc = ma + k;
+        if (mc < lc) lc = mc;
+        if (lc > d.commit) d.commit = lc;
+        ra = 1; rb = ma + k;
+      } break;
+      case M_AE_REP:
+        if (role != R_L || mterm != term) break;
+        mode = SEND_APPEND;
+        if (ma) {
+          peers = on_ack(D, x, me, d, src, mb);
+        } else {
+          uint32_t xx = mb, lo = PR(PF_MATCH, me, src) + 1, hi = d.last + 1;
+          if (xx < lo) xx = lo;
+          if (xx > hi) xx = hi;
+          PR(PF_NEXT, me, src) = xx;
+          peers = 1u << src;
+        }
+        break;
+      case M_IS_REQ: {
+        mode = SEND_REPLY; rtype = M_IS_REP;
+        if (mterm < term) break;  // reply {term, 0}
+        if (role == R_C) d.f = f_set(d.f, 0, 2, R_F);
+        reset_timer(D, x, me, d);
+        uint32_t idx = ma;
+        if (idx > d.commit) {
+          if (!(idx <= d.last && term_at(D, x, me, d, idx) == mb)) d.last = idx;
+          d.snap = idx; d.snapt = mb; NSV(me) = MS64(M64_V, mi);
+          d.commit = idx; d.applied = idx;
+          storage_snapshot(D, x, me, idx);
+          if (x.code != RUN) return;
+          x.cnt[CNT_INSTALLS]++;
+        }
+        rb = idx;
+      } break;
+      case M_IS_REP:
+        if (role == R_L && mterm == term && mb > 0) {
+          mode = SEND_APPEND;
+          peers = on_ack(D, x, me, d, src, mb);
+        }
+        break;
+    }
+  } else if (f_role(d.f) == R_L) {  // heartbeat / replication round
+    kind = 1;
+    set_timer(x, me, x.now + D.hb);
+    mode = SEND_APPEND; peers = others;
+  } else {  // election timeout: become candidate
+    kind = 0;
+    d.term++;
+    d.f = f_set(f_set(f_set(d.f, 4, 4, me), 0, 2, R_C), 16, 8, 1u << me);
+    x.cnt[CNT_ELECTIONS]++;
+    reset_timer(D, x, me, d);
+    mode = SEND_VOTE; peers = others;
   }
-  uint32_t term = ND(NF_TERM, me) + 1;  // election timeout: become candidate
-  ND(NF_TERM, me) = term;
-  ND(NF_FLAGS, me) = f_set(f_set(f_set(f, 4, 4, me), 0, 2, R_C), 16, 8, 1u << me);
-  x.cnt[CNT_ELECTIONS]++;
-  reset_timer(D, x, me);
-  uint32_t last = ND(NF_LAST, me);
-  uint32_t lt = term_at(D, x, me, last, ND(NF_SNAP, me), ND(NF_SNAPT, me));
-  for (uint32_t p = 0; p < D.n; p++) {
-    if (p == me) continue;
-    net_send(D, x, me, p, M_RV_REQ, f_inc(f), term, me, last, lt, 0, 0);
+  if (d.applied < d.commit) {  // committed entries reach the tester's applier
+    node_apply(D, x, me, d);
     if (x.code != RUN) return;
   }
-  rec_node(D, x, 1, 0, me, 0);
+  if (mode == SEND_REPLY) peers = 1u << src;
+  const uint32_t lt = mode == SEND_VOTE ? term_at(D, x, me, d, d.last) : 0u;
+  while (peers) {  // the single send path: ascending peer order
+    uint32_t p = (uint32_t)__builtin_ctz(peers);
+    peers &= peers - 1u;
+    uint32_t st = M_RV_REQ, sa = me, sb = d.last, sc = lt, sk = 0, sinc = f_inc(d.f), prev = 0;
+    uint64_t sv = 0;
+    if (mode == SEND_REPLY) {
+      st = rtype; sa = ra; sb = rb; sc = 0; sinc = inc;
+    } else if (mode == SEND_APPEND) {
+      uint32_t nx = PR(PF_NEXT, me, p);
+      if (nx <= d.snap) {
+        st = M_IS_REQ; sa = d.snap; sb = d.snapt; sc = 0; sv = NSV(me);
+      } else {
+        prev = nx - 1;
+        sk = d.last - prev;
+        if (sk > D.K) sk = D.K;
+        st = M_AE_REQ; sa = prev; sb = term_at(D, x, me, d, prev); sc = d.commit;
+        x.cnt[CNT_SHIPPED] += sk;
+      }
+    }
+    int s = net_send(D, x, me, d, p, st, sinc, d.term, sa, sb, sc, sv, sk);
+    if (x.code != RUN) return;
+    if (s >= 0 && sk) {
+      size_t pb = ((size_t)x.c * D.M + (uint32_t)s) * D.K;
+      for (uint32_t j = 0; j < sk; j++) {
+        size_t li = logi(D, x, me, prev + 1 + j);
+        D.pterm[pb + j] = D.lterm[li];
+        D.pval[pb + j] = D.lval[li];
+      }
+    }
+  }
+  store_node(D, x, me, d);
+  rec_node(D, x, is_msg ? 0u : 1u, kind, me, is_msg ? seq : 0u, d);
 }
 
 // ---------------------------------------------------------------- tester API (tester.rs)
@@ -479,26 +520,25 @@ DI uint64_t t_entry(const Dev& D, X& x) {  // tests.rs:943-951 gen_entry
   return ((uint64_t)w1 << 32) | w0;
 }
 DI void t_set_unrel(X& x, bool u) { x.netmode = (x.netmode & ~1u) | (u ? 1u : 0u); }
-DI bool t_started(const Dev& D, X& x, uint32_t i) { return f_alive(ND(NF_FLAGS, i)); }
-DI bool t_connected(const Dev& D, X& x, uint32_t i) { return f_conn(ND(NF_FLAGS, i)); }
+DI bool t_started(const Dev& D, X& x, uint32_t i) { return bit(x.alive, i); }
+DI bool t_connected(const Dev& D, X& x, uint32_t i) { return bit(x.conn, i); }
 DI void t_conn(const Dev& D, X& x, uint32_t i, uint32_t v) {
-  ND(NF_FLAGS, i) = f_set(ND(NF_FLAGS, i), 3, 1, v);
+  x.conn = v ? (x.conn | (1u << i)) : (x.conn & ~(1u << i));
 }
 DI void t_crash1(const Dev& D, X& x, uint32_t i) {  // tester.rs:329-333
-  ND(NF_FLAGS, i) = f_set(ND(NF_FLAGS, i), 2, 1, 0u);
-  ND(NF_TIMER, i) = INF_T;
+  x.alive &= ~(1u << i);
+  set_timer(x, i, INF_T);
 }
 DI void t_start1(const Dev& D, X& x, uint32_t i) {  // tester.rs:293-327, raft.rs:108-122
   t_crash1(D, x, i);
-  uint32_t f = ND(NF_FLAGS, i);
-  f = f_set(f, 2, 1, 1u);
-  f = f_set(f, 8, 8, f_inc(f) + 1u);
-  f = f_set(f_set(f, 0, 2, R_F), 16, 8, 0u);
-  ND(NF_FLAGS, i) = f;
-  uint32_t snap = ND(NF_SNAP, i);
-  ND(NF_COMMIT, i) = snap;
-  ND(NF_APPLIED, i) = snap;
-  if (!D.null_raft) reset_timer(D, x, i);
+  x.alive |= 1u << i;
+  NC n = load_node(D, x, i);
+  n.f = f_set(n.f, 8, 8, f_inc(n.f) + 1u);
+  n.f = f_set(f_set(n.f, 0, 2, R_F), 16, 8, 0u);
+  n.commit = n.snap;
+  n.applied = n.snap;
+  if (!D.null_raft) reset_timer(D, x, i, n);
+  store_node(D, x, i, n);
 }
 DI void t_new(const Dev& D, X& x, bool snapshot) {  // RaftTester::new, tester.rs:34-60
   x.netmode = (x.netmode & ~2u) | (snapshot ? 2u : 0u);
@@ -507,9 +547,8 @@ DI void t_new(const Dev& D, X& x, bool snapshot) {  // RaftTester::new, tester.r
 }
 // tester.rs:165-171 -> raft.rs:238-244; unwrap() on a crashed raft panics
 DI bool t_start(const Dev& D, X& x, uint32_t i, uint64_t v, uint32_t& idx, uint32_t& term) {
-  uint32_t f = ND(NF_FLAGS, i);
-  if (!f_alive(f)) { fail(D, x, MR_FAIL_UNWRAP_NONE); return false; }
-  if (D.null_raft || f_role(f) != R_L) return false;  // Err(NotLeader((me+1)%n))
+  if (!bit(x.alive, i)) { fail(D, x, MR_FAIL_UNWRAP_NONE); return false; }
+  if (D.null_raft || f_role(ND(NF_FLAGS, i)) != R_L) return false;  // Err(NotLeader((me+1)%n))
   uint32_t snap = ND(NF_SNAP, i), last = ND(NF_LAST, i) + 1;
   if (last - snap > D.log_cap) { fail(D, x, MR_FAIL_SIM_CAPACITY); return false; }
   size_t li = logi(D, x, i, last);
@@ -527,7 +566,7 @@ DI bool t_start(const Dev& D, X& x, uint32_t i, uint64_t v) {
   return t_start(D, x, i, v, a, b);
 }
 DI uint32_t t_term(const Dev& D, X& x, uint32_t i) {
-  if (!f_alive(ND(NF_FLAGS, i))) { fail(D, x, MR_FAIL_UNWRAP_NONE); return 0; }
+  if (!bit(x.alive, i)) { fail(D, x, MR_FAIL_UNWRAP_NONE); return 0; }
   return ND(NF_TERM, i);
 }
 DI uint32_t t_log_size(const Dev& D, X& x) {  // tester.rs:152-158 + SEMANTICS ยง5 size model
@@ -542,9 +581,8 @@ DI uint32_t t_log_size(const Dev& D, X& x) {  // tester.rs:152-158 + SEMANTICS ย
 DI uint32_t t_check_terms(const Dev& D, X& x) {  // tester.rs:95-109
   uint32_t term = 0;
   for (uint32_t i = 0; i < D.n; i++) {
-    uint32_t f = ND(NF_FLAGS, i);
-    if (!f_conn(f)) continue;
-    if (!f_alive(f)) { fail(D, x, MR_FAIL_UNWRAP_NONE); return 0; }
+    if (!bit(x.conn, i)) continue;
+    if (!bit(x.alive, i)) { fail(D, x, MR_FAIL_UNWRAP_NONE); return 0; }
     uint32_t xt = ND(NF_TERM, i);
     if (term == 0) term = xt;
     else if (term != xt) { fail(D, x, MR_FAIL_TERM_DISAGREE); return 0; }
@@ -553,10 +591,12 @@ DI uint32_t t_check_terms(const Dev& D, X& x) {  // tester.rs:95-109
 }
 DI void t_check_no_leader(const Dev& D, X& x) {  // tester.rs:112-122
   for (uint32_t i = 0; i < D.n; i++) {
-    uint32_t f = ND(NF_FLAGS, i);
-    if (!f_conn(f)) continue;
-    if (!f_alive(f)) { fail(D, x, MR_FAIL_UNWRAP_NONE); return; }
-    if (!D.null_raft && f_role(f) == R_L) { fail(D, x, MR_FAIL_UNEXPECTED_LEADER); return; }
+    if (!bit(x.conn, i)) continue;
+    if (!bit(x.alive, i)) { fail(D, x, MR_FAIL_UNWRAP_NONE); return; }
+    if (!D.null_raft && f_role(ND(NF_FLAGS, i)) == R_L) {
+      fail(D, x, MR_FAIL_UNEXPECTED_LEADER);
+      return;
+    }
   }
 }
 DI void t_sleep(X& x, uint32_t us) { x.sleep_us = us; x.yield = 1; }
@@ -581,14 +621,12 @@ DI bool col_step(const Dev& D, X& x, T& t) {
     }
     uint32_t best_term = 0, best = NONE, terms_seen = 0;
     for (uint32_t i = 0; i < D.n; i++) {
-      uint32_t f = ND(NF_FLAGS, i);
-      if (!f_conn(f)) continue;
-      if (!f_alive(f)) { fail(D, x, MR_FAIL_UNWRAP_NONE); return false; }
-      if (D.null_raft || f_role(f) != R_L) continue;
+      if (!bit(x.conn, i)) continue;
+      if (!bit(x.alive, i)) { fail(D, x, MR_FAIL_UNWRAP_NONE); return false; }
+      if (D.null_raft || f_role(ND(NF_FLAGS, i)) != R_L) continue;
       uint32_t ti = ND(NF_TERM, i);
       for (uint32_t j = 0; j < i; j++) {  // >1 leaders in one term?
-        uint32_t g = ND(NF_FLAGS, j);
-        if (f_conn(g) && f_role(g) == R_L && ND(NF_TERM, j) == ti) {
+        if (bit(x.conn, j) && f_role(ND(NF_FLAGS, j)) == R_L && ND(NF_TERM, j) == ti) {
           fail(D, x, MR_FAIL_MULTI_LEADER_TERM);
           return false;
         }
@@ -620,8 +658,7 @@ DI bool one_step(const Dev& D, X& x, T& t) {
       bool have = false;
       for (uint32_t k = 0; k < D.n; k++) {
         starts = (starts + 1) % D.n;
-        uint32_t f = ND(NF_FLAGS, starts);
-        if (!f_conn(f) || !f_alive(f)) continue;
+        if (!bit(x.conn, starts) || !bit(x.alive, starts)) continue;
         if (t_start(D, x, starts, t.hv, index, term)) { have = true; break; }
         if (x.code != RUN) return false;
       }
@@ -657,7 +694,7 @@ DI bool wait_step(const Dev& D, X& x, T& t) {
   if ((t.h[4] & 255u) == 2) {
     if ((t.h[4] >> 16) & 1u) {
       for (uint32_t i = 0; i < D.n; i++)
-        if (f_alive(ND(NF_FLAGS, i)) && ND(NF_TERM, i) > t.h[3]) { t.res = 0; return true; }
+        if (bit(x.alive, i) && ND(NF_TERM, i) > t.h[3]) { t.res = 0; return true; }
     }
     t.h[1]++;
     t.h[4] = (t.h[4] & ~255u) | 1u;
@@ -675,59 +712,56 @@ DI bool wait_step(const Dev& D, X& x, T& t) {
   return true;
 }
 
-// ---- protothreads: the scenario's persistent locals live in t.l[]; a
-// yield stores the frame (pc = the source line) and returns. SLEEP returns to
-// the event loop; AWAIT starts a multi-event tester call and returns to the
-// dispatcher in tester(), which owns the only copy of each call's state
-// machine and resumes the scenario at the same line once the call is done.
+// ---- scenario state machines. Each test body (tests.rs) is split at its
+// suspension points into numbered states; a state ends by sleeping (SLEEP_TO),
+// by starting a multi-event tester call (ONE_TO / COL_TO / WAIT_TO) that the
+// dispatcher in tester() runs before resuming at the given state, by jumping
+// to another state (GO), or with the verdict. The dispatch loop over a switch
+// keeps the control flow reducible (protothread-style resumption into the
+// middle of loops made the AMDGPU structurizer blow up register pressure).
+// Persistent locals live in t.l[].
 enum : uint32_t { H_NONE = 0, H_ONE, H_COL, H_WAIT };
-#define PT_BEGIN switch (t.pc) { case 0:;
-#define PT_END } fail(D, x, MR_FAIL_SIM_BAD_PROGRAM);
 #define CK() do { if (x.code != RUN) return; } while (0)
-#define SLEEP(us) do { t_sleep(x, (us)); t.pc = __LINE__; return; case __LINE__:; } while (0)
-#define AWAIT(init, kind) do { init; t.helper = (kind); t.pc = __LINE__; return; case __LINE__:; } while (0)
-#define ONE(cmd, expected, retry) AWAIT(one_init(D, x, t, (cmd), (expected), (retry)), H_ONE)
-#define CHECK_ONE_LEADER() AWAIT(col_init(t), H_COL)
-#define WAIT(idx, nn, has, st) AWAIT(wait_init(t, (idx), (nn), (has), (st)), H_WAIT)
+#define GO(s) { t.pc = (s); continue; }
+#define SLEEP_TO(us, s) { t_sleep(x, (us)); t.pc = (s); return; }
+#define ONE_TO(cmd, e, r, s) \
+  { one_init(D, x, t, (cmd), (e), (r)); t.helper = H_ONE; t.pc = (s); return; }
+#define COL_TO(s) { col_init(t); t.helper = H_COL; t.pc = (s); return; }
+#define WAIT_TO(idx, nn, has, st, s) \
+  { wait_init(t, (idx), (nn), (has), (st)); t.helper = H_WAIT; t.pc = (s); return; }
+#define END() { t_end(D, x); return; }
+#define BAD() default: fail(D, x, MR_FAIL_SIM_BAD_PROGRAM); return;
 #define TV(k) C64(C64_TV + (k))
 
-// ---------------------------------------------------------------- scenarios (tests.rs)
 DI void scn_initial_election(const Dev& D, X& x, T& t) {  // tests.rs:20-46
-  PT_BEGIN
-  t_new(D, x, false);
-  CHECK_ONE_LEADER();
-  SLEEP(50000);
-  t_check_terms(D, x); CK();
-  SLEEP(2 * ELECTION_US);
-  t_check_terms(D, x); CK();
-  CHECK_ONE_LEADER();
-  t_end(D, x);
-  return;
-  PT_END
+  for (;;) switch (t.pc) {
+    case 0: t_new(D, x, false); COL_TO(1)
+    case 1: SLEEP_TO(50000, 2)
+    case 2: t_check_terms(D, x); CK(); SLEEP_TO(2 * ELECTION_US, 3)
+    case 3: t_check_terms(D, x); CK(); COL_TO(4)  // term1 != term2 only warns
+    case 4: END()
+    BAD()
+  }
 }
 
 DI void scn_reelection(const Dev& D, X& x, T& t) {  // tests.rs:48-78
   const uint32_t n = D.n;
   uint32_t& l1 = t.l[0];
   uint32_t& l2 = t.l[1];
-  PT_BEGIN
-  t_new(D, x, false);
-  CHECK_ONE_LEADER(); l1 = t.res;
-  t_conn(D, x, l1, 0);
-  CHECK_ONE_LEADER();
-  t_conn(D, x, l1, 1);
-  CHECK_ONE_LEADER(); l2 = t.res;
-  t_conn(D, x, l2, 0);
-  t_conn(D, x, (l2 + 1) % n, 0);
-  SLEEP(2 * ELECTION_US);
-  t_check_no_leader(D, x); CK();
-  t_conn(D, x, (l2 + 1) % n, 1);
-  CHECK_ONE_LEADER();
-  t_conn(D, x, l2, 1);
-  CHECK_ONE_LEADER();
-  t_end(D, x);
-  return;
-  PT_END
+  for (;;) switch (t.pc) {
+    case 0: t_new(D, x, false); COL_TO(1)
+    case 1: l1 = t.res; t_conn(D, x, l1, 0); COL_TO(2)
+    case 2: t_conn(D, x, l1, 1); COL_TO(3)
+    case 3:
+      l2 = t.res;
+      t_conn(D, x, l2, 0);
+      t_conn(D, x, (l2 + 1) % n, 0);
+      SLEEP_TO(2 * ELECTION_US, 4)
+    case 4: t_check_no_leader(D, x); CK(); t_conn(D, x, (l2 + 1) % n, 1); COL_TO(5)
+    case 5: t_conn(D, x, l2, 1); COL_TO(6)
+    case 6: END()
+    BAD()
+  }
 }
 
 DI void scn_many_election(const Dev& D, X& x, T& t) {  // tests.rs:80-112
@@ -736,98 +770,98 @@ DI void scn_many_election(const Dev& D, X& x, T& t) {  // tests.rs:80-112
   uint32_t& i1 = t.l[1];
   uint32_t& i2 = t.l[2];
   uint32_t& i3 = t.l[3];
-  PT_BEGIN
-  t_new(D, x, false);
-  CHECK_ONE_LEADER();
-  for (it = 0; it < D.iters; it++) {
-    i1 = t_range(D, x, 0, n); i2 = t_range(D, x, 0, n); i3 = t_range(D, x, 0, n);
-    t_conn(D, x, i1, 0); t_conn(D, x, i2, 0); t_conn(D, x, i3, 0);
-    CHECK_ONE_LEADER();
-    t_conn(D, x, i1, 1); t_conn(D, x, i2, 1); t_conn(D, x, i3, 1);
+  for (;;) switch (t.pc) {
+    case 0: t_new(D, x, false); COL_TO(1)
+    case 1: it = 0; GO(2)
+    case 2:
+      if (it >= D.iters) COL_TO(4)
+      i1 = t_range(D, x, 0, n); i2 = t_range(D, x, 0, n); i3 = t_range(D, x, 0, n);
+      t_conn(D, x, i1, 0); t_conn(D, x, i2, 0); t_conn(D, x, i3, 0);
+      COL_TO(3)
+    case 3:
+      t_conn(D, x, i1, 1); t_conn(D, x, i2, 1); t_conn(D, x, i3, 1);
+      it++;
+      GO(2)
+    case 4: END()
+    BAD()
   }
-  CHECK_ONE_LEADER();
-  t_end(D, x);
-  return;
-  PT_END
 }
 
 DI void scn_basic_agree(const Dev& D, X& x, T& t) {  // tests.rs:114-130
   uint32_t& index = t.l[0];
-  PT_BEGIN
-  t_new(D, x, false);
-  for (index = 1; index <= 3; index++) {
-    {
+  for (;;) switch (t.pc) {
+    case 0: t_new(D, x, false); index = 1; GO(1)
+    case 1: {
+      if (index > 3) END()
       uint64_t v;
       if (n_committed(D, x, index, v) != 0) { fail(D, x, MR_FAIL_BASIC_PRECOMMIT); return; }
+      ONE_TO((uint64_t)index * 100, D.n, false, 2)
     }
-    ONE((uint64_t)index * 100, D.n, false);
-    if (t.res != index) { fail(D, x, MR_FAIL_BASIC_INDEX); return; }
+    case 2:
+      if (t.res != index) { fail(D, x, MR_FAIL_BASIC_INDEX); return; }
+      index++;
+      GO(1)
+    BAD()
   }
-  t_end(D, x);
-  return;
-  PT_END
 }
 
 DI void scn_fail_agree(const Dev& D, X& x, T& t) {  // tests.rs:132-161
   const uint32_t n = D.n;
   uint32_t& leader = t.l[0];
-  PT_BEGIN
-  t_new(D, x, false);
-  ONE(101, n, false);
-  CHECK_ONE_LEADER(); leader = t.res;
-  t_conn(D, x, (leader + 1) % n, 0);
-  ONE(102, n - 1, false);
-  ONE(103, n - 1, false);
-  SLEEP(ELECTION_US);
-  ONE(104, n - 1, false);
-  ONE(105, n - 1, false);
-  t_conn(D, x, (leader + 1) % n, 1);
-  ONE(106, n, true);
-  SLEEP(ELECTION_US);
-  ONE(107, n, true);
-  t_end(D, x);
-  return;
-  PT_END
+  for (;;) switch (t.pc) {
+    case 0: t_new(D, x, false); ONE_TO(101, n, false, 1)
+    case 1: COL_TO(2)
+    case 2: leader = t.res; t_conn(D, x, (leader + 1) % n, 0); ONE_TO(102, n - 1, false, 3)
+    case 3: ONE_TO(103, n - 1, false, 4)
+    case 4: SLEEP_TO(ELECTION_US, 5)
+    case 5: ONE_TO(104, n - 1, false, 6)
+    case 6: ONE_TO(105, n - 1, false, 7)
+    case 7: t_conn(D, x, (leader + 1) % n, 1); ONE_TO(106, n, true, 8)
+    case 8: SLEEP_TO(ELECTION_US, 9)
+    case 9: ONE_TO(107, n, true, 10)
+    case 10: END()
+    BAD()
+  }
 }
 
 DI void scn_fail_no_agree(const Dev& D, X& x, T& t) {  // tests.rs:163-209
   const uint32_t n = D.n;
   uint32_t& leader = t.l[0];
   uint32_t& index = t.l[1];
-  PT_BEGIN
-  t_new(D, x, false);
-  ONE(10, n, false);
-  CHECK_ONE_LEADER(); leader = t.res;
-  t_conn(D, x, (leader + 1) % n, 0);
-  t_conn(D, x, (leader + 2) % n, 0);
-  t_conn(D, x, (leader + 3) % n, 0);
-  {
-    uint32_t term;
-    bool ok = t_start(D, x, leader, 20, index, term);
-    CK();
-    if (!ok) { fail(D, x, MR_FAIL_LEADER_REJECTED); return; }
+  for (;;) switch (t.pc) {
+    case 0: t_new(D, x, false); ONE_TO(10, n, false, 1)
+    case 1: COL_TO(2)
+    case 2: {
+      leader = t.res;
+      t_conn(D, x, (leader + 1) % n, 0);
+      t_conn(D, x, (leader + 2) % n, 0);
+      t_conn(D, x, (leader + 3) % n, 0);
+      uint32_t term;
+      bool ok = t_start(D, x, leader, 20, index, term);
+      CK();
+      if (!ok) { fail(D, x, MR_FAIL_LEADER_REJECTED); return; }
+      if (index != 2) { fail(D, x, MR_FAIL_EXPECTED_INDEX2); return; }
+      SLEEP_TO(2 * ELECTION_US, 3)
+    }
+    case 3: {
+      uint64_t v;
+      if (n_committed(D, x, index, v) != 0) { fail(D, x, MR_FAIL_NO_MAJORITY_COMMIT); return; }
+      t_conn(D, x, (leader + 1) % n, 1);
+      t_conn(D, x, (leader + 2) % n, 1);
+      t_conn(D, x, (leader + 3) % n, 1);
+      COL_TO(4)
+    }
+    case 4: {
+      uint32_t idx2, term;
+      bool ok = t_start(D, x, t.res, 30, idx2, term);
+      CK();
+      if (!ok) { fail(D, x, MR_FAIL_LEADER_REJECTED); return; }
+      if (idx2 < 2 || idx2 > 3) { fail(D, x, MR_FAIL_UNEXPECTED_INDEX); return; }
+      ONE_TO(1000, n, true, 5)
+    }
+    case 5: END()
+    BAD()
   }
-  if (index != 2) { fail(D, x, MR_FAIL_EXPECTED_INDEX2); return; }
-  SLEEP(2 * ELECTION_US);
-  {
-    uint64_t v;
-    if (n_committed(D, x, index, v) != 0) { fail(D, x, MR_FAIL_NO_MAJORITY_COMMIT); return; }
-  }
-  t_conn(D, x, (leader + 1) % n, 1);
-  t_conn(D, x, (leader + 2) % n, 1);
-  t_conn(D, x, (leader + 3) % n, 1);
-  CHECK_ONE_LEADER();
-  {
-    uint32_t idx2, term;
-    bool ok = t_start(D, x, t.res, 30, idx2, term);
-    CK();
-    if (!ok) { fail(D, x, MR_FAIL_LEADER_REJECTED); return; }
-    if (idx2 < 2 || idx2 > 3) { fail(D, x, MR_FAIL_UNEXPECTED_INDEX); return; }
-  }
-  ONE(1000, n, true);
-  t_end(D, x);
-  return;
-  PT_END
 }
 
 // (0..servers).any(|j| t.term(j) != term) with unwrap() semantics
@@ -844,72 +878,73 @@ DI void scn_concurrent_starts(const Dev& D, X& x, T& t) {  // tests.rs:211-275
   const uint32_t n = D.n;
   uint32_t& tried = t.l[0];
   uint32_t& term = t.l[1];
-  uint32_t& ni = t.l[2];   // idxes in TV(0..5)
+  uint32_t& ni = t.l[2];  // idxes in TV(0..5)
   uint32_t& q = t.l[3];
-  uint32_t& nc = t.l[4];   // cmds in TV(8..13)
-  PT_BEGIN
-  t_new(D, x, false);
-  for (tried = 0; tried < 5; tried++) {
-    if (tried > 0) SLEEP(3000000);
-    CHECK_ONE_LEADER();
-    {
+  uint32_t& nc = t.l[4];  // cmds in TV(8..13)
+  for (;;) switch (t.pc) {
+    case 0: t_new(D, x, false); tried = 0; GO(1)
+    case 1:
+      if (tried >= 5) { fail(D, x, MR_FAIL_TERM_CHANGED); return; }  // assert!(success)
+      if (tried > 0) SLEEP_TO(3000000, 2)
+      GO(2)
+    case 2: COL_TO(3)
+    case 3: {
       uint32_t leader = t.res, idx, st;
       bool ok = t_start(D, x, leader, 1, idx, term);
       CK();
-      if (!ok) continue;
+      if (!ok) { tried++; GO(1) }
       ni = 0;
       for (uint32_t ii = 0; ii < 5; ii++) {
         bool ok2 = t_start(D, x, leader, 100 + ii, idx, st);
         CK();
         if (ok2 && st == term) { TV(ni) = idx; ni++; }
       }
-    }
-    {
       bool ch = any_term_changed(D, x, term);
       CK();
-      if (ch) continue;
+      if (ch) { tried++; GO(1) }
+      nc = 0;
+      q = 0;
+      GO(4)
     }
-    nc = 0;
-    for (q = 0; q < ni; q++) {
-      WAIT((uint32_t)TV(q), n, true, term);
+    case 4:
+      if (q >= ni) GO(6)
+      WAIT_TO((uint32_t)TV(q), n, true, term, 5)
+    case 5:
       if (t.res) { TV(8 + nc) = t.hv; nc++; }
-    }
-    for (uint32_t ii = 0; ii < 5; ii++) {
-      bool ok = false;
-      for (uint32_t k = 0; k < nc; k++)
-        if (TV(8 + k) == 100 + ii) ok = true;
-      if (!ok) { fail(D, x, MR_FAIL_CMD_MISSING); return; }
-    }
-    t_end(D, x);  // success -> break; assert!(success); t.end()
-    return;
+      q++;
+      GO(4)
+    case 6:
+      for (uint32_t ii = 0; ii < 5; ii++) {
+        bool ok = false;
+        for (uint32_t k = 0; k < nc; k++)
+          if (TV(8 + k) == 100 + ii) ok = true;
+        if (!ok) { fail(D, x, MR_FAIL_CMD_MISSING); return; }
+      }
+      END()
+    BAD()
   }
-  fail(D, x, MR_FAIL_TERM_CHANGED);
-  return;
-  PT_END
 }
 
 DI void scn_rejoin(const Dev& D, X& x, T& t) {  // tests.rs:277-313
   const uint32_t n = D.n;
   uint32_t& l1 = t.l[0];
   uint32_t& l2 = t.l[1];
-  PT_BEGIN
-  t_new(D, x, false);
-  ONE(101, n, true);
-  CHECK_ONE_LEADER(); l1 = t.res;
-  t_conn(D, x, l1, 0);
-  t_start(D, x, l1, 102); CK();
-  t_start(D, x, l1, 103); CK();
-  t_start(D, x, l1, 104); CK();
-  ONE(103, 2, true);
-  CHECK_ONE_LEADER(); l2 = t.res;
-  t_conn(D, x, l2, 0);
-  t_conn(D, x, l1, 1);
-  ONE(104, 2, true);
-  t_conn(D, x, l2, 1);
-  ONE(105, n, true);
-  t_end(D, x);
-  return;
-  PT_END
+  for (;;) switch (t.pc) {
+    case 0: t_new(D, x, false); ONE_TO(101, n, true, 1)
+    case 1: COL_TO(2)
+    case 2:
+      l1 = t.res;
+      t_conn(D, x, l1, 0);
+      t_start(D, x, l1, 102); CK();
+      t_start(D, x, l1, 103); CK();
+      t_start(D, x, l1, 104); CK();
+      ONE_TO(103, 2, true, 3)
+    case 3: COL_TO(4)
+    case 4: l2 = t.res; t_conn(D, x, l2, 0); t_conn(D, x, l1, 1); ONE_TO(104, 2, true, 5)
+    case 5: t_conn(D, x, l2, 1); ONE_TO(105, n, true, 6)
+    case 6: END()
+    BAD()
+  }
 }
 
 DI void scn_backup(const Dev& D, X& x, T& t) {  // tests.rs:315-386
@@ -918,36 +953,51 @@ DI void scn_backup(const Dev& D, X& x, T& t) {  // tests.rs:315-386
   uint32_t& l2 = t.l[1];
   uint32_t& other = t.l[2];
   uint32_t& i = t.l[3];
-  PT_BEGIN
-  t_new(D, x, false);
-  ONE(t_entry(D, x), n, true);
-  CHECK_ONE_LEADER(); l1 = t.res;
-  t_conn(D, x, (l1 + 2) % n, 0); t_conn(D, x, (l1 + 3) % n, 0); t_conn(D, x, (l1 + 4) % n, 0);
-  for (uint32_t k = 0; k < 50; k++) {
-    uint64_t e = t_entry(D, x);
-    t_start(D, x, l1, e); CK();
+  for (;;) switch (t.pc) {
+    case 0: t_new(D, x, false); ONE_TO(t_entry(D, x), n, true, 1)
+    case 1: COL_TO(2)
+    case 2:
+      l1 = t.res;
+      t_conn(D, x, (l1 + 2) % n, 0); t_conn(D, x, (l1 + 3) % n, 0); t_conn(D, x, (l1 + 4) % n, 0);
+      for (uint32_t k = 0; k < 50; k++) {
+        uint64_t e = t_entry(D, x);
+        t_start(D, x, l1, e); CK();
+      }
+      SLEEP_TO(ELECTION_US / 2, 3)
+    case 3:
+      t_conn(D, x, (l1 + 0) % n, 0); t_conn(D, x, (l1 + 1) % n, 0);
+      t_conn(D, x, (l1 + 2) % n, 1); t_conn(D, x, (l1 + 3) % n, 1); t_conn(D, x, (l1 + 4) % n, 1);
+      i = 0;
+      GO(4)
+    case 4:
+      if (i >= 50) COL_TO(6)
+      ONE_TO(t_entry(D, x), 3, true, 5)
+    case 5: i++; GO(4)
+    case 6:
+      l2 = t.res;
+      other = (l1 + 2) % n;
+      if (l2 == other) other = (l2 + 1) % n;
+      t_conn(D, x, other, 0);
+      for (uint32_t k = 0; k < 50; k++) {
+        uint64_t e = t_entry(D, x);
+        t_start(D, x, l2, e); CK();
+      }
+      SLEEP_TO(ELECTION_US / 2, 7)
+    case 7:
+      for (uint32_t k = 0; k < n; k++) t_conn(D, x, k, 0);
+      t_conn(D, x, (l1 + 0) % n, 1); t_conn(D, x, (l1 + 1) % n, 1); t_conn(D, x, other, 1);
+      i = 0;
+      GO(8)
+    case 8:
+      if (i >= 50) {
+        for (uint32_t k = 0; k < n; k++) t_conn(D, x, k, 1);
+        ONE_TO(t_entry(D, x), n, true, 10)
+      }
+      ONE_TO(t_entry(D, x), 3, true, 9)
+    case 9: i++; GO(8)
+    case 10: END()
+    BAD()
   }
-  SLEEP(ELECTION_US / 2);
-  t_conn(D, x, (l1 + 0) % n, 0); t_conn(D, x, (l1 + 1) % n, 0);
-  t_conn(D, x, (l1 + 2) % n, 1); t_conn(D, x, (l1 + 3) % n, 1); t_conn(D, x, (l1 + 4) % n, 1);
-  for (i = 0; i < 50; i++) ONE(t_entry(D, x), 3, true);
-  CHECK_ONE_LEADER(); l2 = t.res;
-  other = (l1 + 2) % n;
-  if (l2 == other) other = (l2 + 1) % n;
-  t_conn(D, x, other, 0);
-  for (uint32_t k = 0; k < 50; k++) {
-    uint64_t e = t_entry(D, x);
-    t_start(D, x, l2, e); CK();
-  }
-  SLEEP(ELECTION_US / 2);
-  for (uint32_t k = 0; k < n; k++) t_conn(D, x, k, 0);
-  t_conn(D, x, (l1 + 0) % n, 1); t_conn(D, x, (l1 + 1) % n, 1); t_conn(D, x, other, 1);
-  for (i = 0; i < 50; i++) ONE(t_entry(D, x), 3, true);
-  for (uint32_t k = 0; k < n; k++) t_conn(D, x, k, 1);
-  ONE(t_entry(D, x), n, true);
-  t_end(D, x);
-  return;
-  PT_END
 }
 
 DI void scn_count(const Dev& D, X& x, T& t) {  // tests.rs:388-479
@@ -958,21 +1008,25 @@ DI void scn_count(const Dev& D, X& x, T& t) {  // tests.rs:388-479
   uint32_t& starti = t.l[3];
   uint32_t& term = t.l[4];
   uint32_t& i = t.l[5];
-  PT_BEGIN
-  t_new(D, x, false);
-  CHECK_ONE_LEADER();
-  total1 = x.msgs_sent / 2;
-  if (total1 < 1 || total1 > 30) { fail(D, x, MR_FAIL_RPC_INITIAL); return; }
-  total2 = 0;
-  for (tried = 0; tried < 5; tried++) {
-    if (tried > 0) SLEEP(3000000);
-    CHECK_ONE_LEADER();
-    total1 = x.msgs_sent / 2;
-    {
+  for (;;) switch (t.pc) {
+    case 0: t_new(D, x, false); COL_TO(1)
+    case 1:
+      total1 = x.msgs_sent / 2;
+      if (total1 < 1 || total1 > 30) { fail(D, x, MR_FAIL_RPC_INITIAL); return; }
+      total2 = 0;
+      tried = 0;
+      GO(2)
+    case 2:
+      if (tried >= 5) { fail(D, x, MR_FAIL_TERM_CHANGED); return; }
+      if (tried > 0) SLEEP_TO(3000000, 3)
+      GO(3)
+    case 3: COL_TO(4)
+    case 4: {
+      total1 = x.msgs_sent / 2;
       uint32_t leader = t.res, idx, st;
       bool ok = t_start(D, x, leader, 1, starti, term);
       CK();
-      if (!ok) continue;
+      if (!ok) { tried++; GO(2) }
       bool outer = false;
       for (uint32_t k = 1; k < 10 + 2; k++) {
         uint64_t xv = t_entry(D, x);  // random.gen::<u64>()
@@ -982,54 +1036,55 @@ DI void scn_count(const Dev& D, X& x, T& t) {  // tests.rs:388-479
         if (!ok2 || st != term) { outer = true; break; }
         if (starti + k != idx) { fail(D, x, MR_FAIL_START_FAILED); return; }
       }
-      if (outer) continue;
+      if (outer) { tried++; GO(2) }
+      i = 1;
+      GO(5)
     }
-    for (i = 1; i <= 10; i++) {
-      WAIT(starti + i, n, true, term);
+    case 5:
+      if (i > 10) GO(7)
+      WAIT_TO(starti + i, n, true, term, 6)
+    case 6:
       if (t.res && t.hv != TV(i - 1)) { fail(D, x, MR_FAIL_WRONG_VALUE); return; }
-    }
-    {
+      i++;
+      GO(5)
+    case 7: {
       bool ch = any_term_changed(D, x, term);
       CK();
-      if (ch) continue;
+      if (ch) { tried++; GO(2) }
+      total2 = x.msgs_sent / 2;
+      if (total2 - total1 > (10 + 1 + 3) * 3) { fail(D, x, MR_FAIL_RPC_TOO_MANY); return; }
+      SLEEP_TO(ELECTION_US, 8)
     }
-    total2 = x.msgs_sent / 2;
-    if (total2 - total1 > (10 + 1 + 3) * 3) { fail(D, x, MR_FAIL_RPC_TOO_MANY); return; }
-    break;
+    case 8:
+      if (x.msgs_sent / 2 - total2 > 3 * 20) { fail(D, x, MR_FAIL_RPC_IDLE); return; }
+      END()
+    BAD()
   }
-  if (tried >= 5) { fail(D, x, MR_FAIL_TERM_CHANGED); return; }
-  SLEEP(ELECTION_US);
-  if (x.msgs_sent / 2 - total2 > 3 * 20) { fail(D, x, MR_FAIL_RPC_IDLE); return; }
-  t_end(D, x);
-  return;
-  PT_END
 }
 
 DI void scn_persist1(const Dev& D, X& x, T& t) {  // tests.rs:481-526
   const uint32_t n = D.n;
   uint32_t& l = t.l[0];
-  PT_BEGIN
-  t_new(D, x, false);
-  ONE(11, n, true);
-  for (uint32_t i = 0; i < n; i++) t_start1(D, x, i);
-  for (uint32_t i = 0; i < n; i++) { t_conn(D, x, i, 0); t_conn(D, x, i, 1); }
-  ONE(12, n, true);
-  CHECK_ONE_LEADER(); l = t.res;
-  t_conn(D, x, l, 0); t_start1(D, x, l); t_conn(D, x, l, 1);
-  ONE(13, n, true);
-  CHECK_ONE_LEADER(); l = t.res;
-  t_conn(D, x, l, 0);
-  ONE(14, n - 1, true);
-  t_start1(D, x, l); t_conn(D, x, l, 1);
-  WAIT(4, n, false, 0);
-  CHECK_ONE_LEADER(); l = (t.res + 1) % n;
-  t_conn(D, x, l, 0);
-  ONE(15, n - 1, true);
-  t_start1(D, x, l); t_conn(D, x, l, 1);
-  ONE(16, n, true);
-  t_end(D, x);
-  return;
-  PT_END
+  for (;;) switch (t.pc) {
+    case 0: t_new(D, x, false); ONE_TO(11, n, true, 1)
+    case 1:
+      for (uint32_t i = 0; i < n; i++) t_start1(D, x, i);
+      for (uint32_t i = 0; i < n; i++) { t_conn(D, x, i, 0); t_conn(D, x, i, 1); }
+      ONE_TO(12, n, true, 2)
+    case 2: COL_TO(3)
+    case 3:
+      l = t.res;
+      t_conn(D, x, l, 0); t_start1(D, x, l); t_conn(D, x, l, 1);
+      ONE_TO(13, n, true, 4)
+    case 4: COL_TO(5)
+    case 5: l = t.res; t_conn(D, x, l, 0); ONE_TO(14, n - 1, true, 6)
+    case 6: t_start1(D, x, l); t_conn(D, x, l, 1); WAIT_TO(4, n, false, 0, 7)
+    case 7: COL_TO(8)
+    case 8: l = (t.res + 1) % n; t_conn(D, x, l, 0); ONE_TO(15, n - 1, true, 9)
+    case 9: t_start1(D, x, l); t_conn(D, x, l, 1); ONE_TO(16, n, true, 10)
+    case 10: END()
+    BAD()
+  }
 }
 
 DI void scn_persist2(const Dev& D, X& x, T& t) {  // tests.rs:528-572
@@ -1037,46 +1092,53 @@ DI void scn_persist2(const Dev& D, X& x, T& t) {  // tests.rs:528-572
   uint32_t& index = t.l[0];
   uint32_t& k = t.l[1];
   uint32_t& l1 = t.l[2];
-  PT_BEGIN
-  t_new(D, x, false);
-  index = 1;
-  for (k = 0; k < 5; k++) {
-    ONE(10 + index, n, true); index++;
-    CHECK_ONE_LEADER(); l1 = t.res;
-    t_conn(D, x, (l1 + 1) % n, 0); t_conn(D, x, (l1 + 2) % n, 0);
-    ONE(10 + index, n - 2, true); index++;
-    t_conn(D, x, (l1 + 0) % n, 0); t_conn(D, x, (l1 + 3) % n, 0); t_conn(D, x, (l1 + 4) % n, 0);
-    t_start1(D, x, (l1 + 1) % n); t_start1(D, x, (l1 + 2) % n);
-    t_conn(D, x, (l1 + 1) % n, 1); t_conn(D, x, (l1 + 2) % n, 1);
-    SLEEP(ELECTION_US);
-    t_start1(D, x, (l1 + 3) % n); t_conn(D, x, (l1 + 3) % n, 1);
-    ONE(10 + index, n - 2, true); index++;
-    t_conn(D, x, (l1 + 4) % n, 1); t_conn(D, x, (l1 + 0) % n, 1);
+  for (;;) switch (t.pc) {
+    case 0: t_new(D, x, false); index = 1; k = 0; GO(1)
+    case 1:
+      if (k >= 5) ONE_TO(1000, n, true, 7)
+      ONE_TO(10 + index, n, true, 2)
+    case 2: index++; COL_TO(3)
+    case 3:
+      l1 = t.res;
+      t_conn(D, x, (l1 + 1) % n, 0); t_conn(D, x, (l1 + 2) % n, 0);
+      ONE_TO(10 + index, n - 2, true, 4)
+    case 4:
+      index++;
+      t_conn(D, x, (l1 + 0) % n, 0); t_conn(D, x, (l1 + 3) % n, 0); t_conn(D, x, (l1 + 4) % n, 0);
+      t_start1(D, x, (l1 + 1) % n); t_start1(D, x, (l1 + 2) % n);
+      t_conn(D, x, (l1 + 1) % n, 1); t_conn(D, x, (l1 + 2) % n, 1);
+      SLEEP_TO(ELECTION_US, 5)
+    case 5:
+      t_start1(D, x, (l1 + 3) % n); t_conn(D, x, (l1 + 3) % n, 1);
+      ONE_TO(10 + index, n - 2, true, 6)
+    case 6:
+      index++;
+      t_conn(D, x, (l1 + 4) % n, 1); t_conn(D, x, (l1 + 0) % n, 1);
+      k++;
+      GO(1)
+    case 7: END()
+    BAD()
   }
-  ONE(1000, n, true);
-  t_end(D, x);
-  return;
-  PT_END
 }
 
 DI void scn_persist3(const Dev& D, X& x, T& t) {  // tests.rs:574-602
   const uint32_t n = D.n;
   uint32_t& leader = t.l[0];
-  PT_BEGIN
-  t_new(D, x, false);
-  ONE(101, 3, true);
-  CHECK_ONE_LEADER(); leader = t.res;
-  t_conn(D, x, (leader + 2) % n, 0);
-  ONE(102, 2, true);
-  t_crash1(D, x, (leader + 0) % n); t_crash1(D, x, (leader + 1) % n);
-  t_conn(D, x, (leader + 2) % n, 1);
-  t_start1(D, x, (leader + 0) % n); t_conn(D, x, (leader + 0) % n, 1);
-  ONE(103, 2, true);
-  t_start1(D, x, (leader + 1) % n); t_conn(D, x, (leader + 1) % n, 1);
-  ONE(104, n, true);
-  t_end(D, x);
-  return;
-  PT_END
+  for (;;) switch (t.pc) {
+    case 0: t_new(D, x, false); ONE_TO(101, 3, true, 1)
+    case 1: COL_TO(2)
+    case 2: leader = t.res; t_conn(D, x, (leader + 2) % n, 0); ONE_TO(102, 2, true, 3)
+    case 3:
+      t_crash1(D, x, (leader + 0) % n); t_crash1(D, x, (leader + 1) % n);
+      t_conn(D, x, (leader + 2) % n, 1);
+      t_start1(D, x, (leader + 0) % n); t_conn(D, x, (leader + 0) % n, 1);
+      ONE_TO(103, 2, true, 4)
+    case 4:
+      t_start1(D, x, (leader + 1) % n); t_conn(D, x, (leader + 1) % n, 1);
+      ONE_TO(104, n, true, 5)
+    case 5: END()
+    BAD()
+  }
 }
 
 DI uint32_t fig8_delay(const Dev& D, X& x) {  // tests.rs:631-635 / 711-715
@@ -1090,33 +1152,38 @@ DI void scn_figure_8(const Dev& D, X& x, T& t, bool unreliable) {
   uint32_t& nup = t.l[0];
   uint32_t& it = t.l[1];
   uint32_t& leader = t.l[2];
-  PT_BEGIN
-  t_new(D, x, false);
-  if (unreliable) t_set_unrel(x, true);
-  ONE(t_entry(D, x), 1, true);
-  nup = n;
-  for (it = 0; it < D.iters; it++) {
-    leader = NONE;
-    for (uint32_t i = 0; i < n; i++) {
-      if (!t_started(D, x, i)) continue;
-      uint64_t e = t_entry(D, x);
-      bool ok = t_start(D, x, i, e);
-      CK();
-      if (ok) leader = i;
-    }
-    SLEEP(fig8_delay(D, x));
-    if (leader != NONE) { t_crash1(D, x, leader); nup--; }
-    if (nup < 3) {
-      uint32_t s = t_range(D, x, 0, n);
-      if (!t_started(D, x, s)) { t_start1(D, x, s); nup++; }
-    }
+  for (;;) switch (t.pc) {
+    case 0:
+      t_new(D, x, false);
+      if (unreliable) t_set_unrel(x, true);
+      ONE_TO(t_entry(D, x), 1, true, 1)
+    case 1: nup = n; it = 0; GO(2)
+    case 2:
+      if (it >= D.iters) {
+        for (uint32_t i = 0; i < n; i++)
+          if (!t_started(D, x, i)) t_start1(D, x, i);
+        ONE_TO(t_entry(D, x), n, true, 4)
+      }
+      leader = NONE;
+      for (uint32_t i = 0; i < n; i++) {
+        if (!t_started(D, x, i)) continue;
+        uint64_t e = t_entry(D, x);
+        bool ok = t_start(D, x, i, e);
+        CK();
+        if (ok) leader = i;
+      }
+      SLEEP_TO(fig8_delay(D, x), 3)
+    case 3:
+      if (leader != NONE) { t_crash1(D, x, leader); nup--; }
+      if (nup < 3) {
+        uint32_t s = t_range(D, x, 0, n);
+        if (!t_started(D, x, s)) { t_start1(D, x, s); nup++; }
+      }
+      it++;
+      GO(2)
+    case 4: END()
+    BAD()
   }
-  for (uint32_t i = 0; i < n; i++)
-    if (!t_started(D, x, i)) t_start1(D, x, i);
-  ONE(t_entry(D, x), n, true);
-  t_end(D, x);
-  return;
-  PT_END
 }
 
 DI void scn_figure_8_unreliable(const Dev& D, X& x, T& t) {  // tests.rs:688-741
@@ -1124,34 +1191,39 @@ DI void scn_figure_8_unreliable(const Dev& D, X& x, T& t) {  // tests.rs:688-741
   uint32_t& nup = t.l[0];
   uint32_t& it = t.l[1];
   uint32_t& leader = t.l[2];
-  PT_BEGIN
-  t_new(D, x, false);
-  t_set_unrel(x, true);
-  ONE(t_entry(D, x), 1, true);
-  nup = n;
-  for (it = 0; it < D.iters; it++) {
-    leader = NONE;
-    for (uint32_t i = 0; i < n; i++) {
-      uint64_t e = t_entry(D, x);
-      bool ok = t_start(D, x, i, e);
-      CK();
-      if (ok && t_connected(D, x, i)) leader = i;
-    }
-    SLEEP(fig8_delay(D, x));
-    if (leader != NONE && t_range(D, x, 0, 1000) < ELECTION_US / 1000 / 2) {
-      t_conn(D, x, leader, 0);
-      nup--;
-    }
-    if (nup < 3) {
-      uint32_t s = t_range(D, x, 0, n);
-      if (!t_connected(D, x, s)) { t_conn(D, x, s, 1); nup++; }
-    }
+  for (;;) switch (t.pc) {
+    case 0:
+      t_new(D, x, false);
+      t_set_unrel(x, true);
+      ONE_TO(t_entry(D, x), 1, true, 1)
+    case 1: nup = n; it = 0; GO(2)
+    case 2:
+      if (it >= D.iters) {
+        for (uint32_t i = 0; i < n; i++) t_conn(D, x, i, 1);
+        ONE_TO(t_entry(D, x), n, true, 4)
+      }
+      leader = NONE;
+      for (uint32_t i = 0; i < n; i++) {
+        uint64_t e = t_entry(D, x);
+        bool ok = t_start(D, x, i, e);
+        CK();
+        if (ok && t_connected(D, x, i)) leader = i;
+      }
+      SLEEP_TO(fig8_delay(D, x), 3)
+    case 3:
+      if (leader != NONE && t_range(D, x, 0, 1000) < ELECTION_US / 1000 / 2) {
+        t_conn(D, x, leader, 0);
+        nup--;
+      }
+      if (nup < 3) {
+        uint32_t s = t_range(D, x, 0, n);
+        if (!t_connected(D, x, s)) { t_conn(D, x, s, 1); nup++; }
+      }
+      it++;
+      GO(2)
+    case 4: END()
+    BAD()
   }
-  for (uint32_t i = 0; i < n; i++) t_conn(D, x, i, 1);
-  ONE(t_entry(D, x), n, true);
-  t_end(D, x);
-  return;
-  PT_END
 }
 
 DI void scn_snap_common(const Dev& D, X& x, T& t, bool disconnect, bool reliable, bool crash) {
@@ -1160,50 +1232,50 @@ DI void scn_snap_common(const Dev& D, X& x, T& t, bool disconnect, bool reliable
   uint32_t& leader1 = t.l[0];
   uint32_t& i = t.l[1];
   uint32_t& victim = t.l[2];
-  PT_BEGIN
-  t_new(D, x, true);
-  t_set_unrel(x, !reliable);
-  ONE(t_entry(D, x), n, true);
-  CHECK_ONE_LEADER(); leader1 = t.res;
-  for (i = 0; i < D.iters; i++) {
-    victim = (leader1 + 1) % n;
-    if (i % 3 == 1) victim = leader1;
-    if (disconnect) {
-      t_conn(D, x, victim, 0);
-      ONE(t_entry(D, x), n - 1, true);
-    }
-    if (crash) {
-      t_crash1(D, x, victim);
-      ONE(t_entry(D, x), n - 1, true);
-    }
-    {
+  for (;;) switch (t.pc) {
+    case 0:
+      t_new(D, x, true);
+      t_set_unrel(x, !reliable);
+      ONE_TO(t_entry(D, x), n, true, 1)
+    case 1: COL_TO(2)
+    case 2: leader1 = t.res; i = 0; GO(3)
+    case 3:
+      if (i >= D.iters) END()
+      victim = (i % 3 == 1) ? leader1 : (leader1 + 1) % n;
+      if (disconnect) { t_conn(D, x, victim, 0); ONE_TO(t_entry(D, x), n - 1, true, 4) }
+      GO(4)
+    case 4:
+      if (crash) { t_crash1(D, x, victim); ONE_TO(t_entry(D, x), n - 1, true, 5) }
+      GO(5)
+    case 5: {
       uint32_t sender = (i % 3 == 1) ? (leader1 + 1) % n : leader1;
       for (uint32_t k = 0; k <= 10; k++) {  // send enough to get a snapshot
         uint64_t e = t_entry(D, x);
         t_start(D, x, sender, e);
         CK();
       }
+      ONE_TO(t_entry(D, x), n - 1, true, 6)
     }
-    ONE(t_entry(D, x), n - 1, true);
-    if (t_log_size(D, x) >= 2000) { fail(D, x, MR_FAIL_LOG_SIZE); return; }
-    if (disconnect) {
-      t_conn(D, x, victim, 1);
-      ONE(t_entry(D, x), n, true);
-      CHECK_ONE_LEADER(); leader1 = t.res;
-    }
-    if (crash) {
-      t_start1(D, x, victim);
-      t_conn(D, x, victim, 1);
-      ONE(t_entry(D, x), n, true);
-      CHECK_ONE_LEADER(); leader1 = t.res;
-    }
+    case 6:
+      if (t_log_size(D, x) >= 2000) { fail(D, x, MR_FAIL_LOG_SIZE); return; }
+      if (disconnect) { t_conn(D, x, victim, 1); ONE_TO(t_entry(D, x), n, true, 7) }
+      GO(9)
+    case 7: COL_TO(8)
+    case 8: leader1 = t.res; GO(9)
+    case 9:
+      if (crash) {
+        t_start1(D, x, victim);
+        t_conn(D, x, victim, 1);
+        ONE_TO(t_entry(D, x), n, true, 10)
+      }
+      GO(12)
+    case 10: COL_TO(11)
+    case 11: leader1 = t.res; GO(12)
+    case 12: i++; GO(3)
+    BAD()
   }
-  t_end(D, x);
-  return;
-  PT_END
 }
 
-// one tester event: resume the cluster's coroutine until it sleeps or ends
 DI void run_scenario(const Dev& D, X& x, T& t) {
   switch (D.scenario) {
     case MR_SCN_INITIAL_ELECTION_2A: scn_initial_election(D, x, t); break;
@@ -1289,6 +1361,9 @@ __global__ void __launch_bounds__(256, MR_WAVES_PER_EU) step_kernel(Dev D, uint3
     x.now = CS(CS_NOW); x.events = CS(CS_EVENTS); x.msgs_sent = CS(CS_MSGS);
     x.inflight = CS(CS_INFLIGHT); x.trace_n = CS(CS_TRACEN); x.mslot = CS(CS_MSLOT);
     x.netmode = CS(CS_NETMODE); x.t_ctr = CS(CS_TCTR);
+    x.conn = CS(CS_CONN); x.alive = CS(CS_ALIVE);
+#pragma unroll
+    for (uint32_t d = 0; d < MR_MAX_NODES; d++) x.timer[d] = d < D.n ? ND(NF_TIMER, d) : INF_T;
     x.free_mask = C64(C64_FREE); x.digest = C64(C64_DIGEST); x.mmin = C64(C64_MMIN);
 #pragma unroll
     for (uint32_t k = 0; k < CNT__N; k++) x.cnt[k] = CS(CS_CNT + k);
@@ -1298,13 +1373,15 @@ __global__ void __launch_bounds__(256, MR_WAVES_PER_EU) step_kernel(Dev D, uint3
   uint32_t cls = CLS_NONE, node = 0;
   bool need = true;
   for (uint32_t it = 0; it < budget; it++) {
+    asm volatile("" : "+v"(x.c));  // no LICM of per-lane addresses: recompute, do not keep live
     const bool run = x.code == RUN;
     if (__ballot(run) == 0) break;
     if (run && need) {  // next event: min over tester wake-up, node timers, earliest message
       key = ((uint64_t)CS(CS_TWAKE) << 32) | (2ull << 30);
       cls = CLS_TESTER;
-      for (uint32_t d = 0; d < D.n; d++) {
-        uint64_t kt = ((uint64_t)ND(NF_TIMER, d) << 32) | (1ull << 30) | d;
+#pragma unroll
+      for (uint32_t d = 0; d < MR_MAX_NODES; d++) {  // timers of absent nodes are INF_T
+        uint64_t kt = ((uint64_t)x.timer[d] << 32) | (1ull << 30) | d;
         if (kt < key) { key = kt; cls = CLS_TIMER; node = d; }
       }
       if (x.mmin < key) { key = x.mmin; cls = CLS_MSG; }
@@ -1320,12 +1397,9 @@ __global__ void __launch_bounds__(256, MR_WAVES_PER_EU) step_kernel(Dev D, uint3
     need = true;
     x.events++;
     if (x.events > D.max_events) { fail(D, x, MR_FAIL_SIM_EVENT_LIMIT); continue; }
-    if (pick == CLS_MSG) {
-      x.cnt[CNT_EV_MSG]++;
-      deliver(D, x, x.mslot, (uint32_t)key & 0x3FFFFFFFu);
-    } else if (pick == CLS_TIMER) {
-      x.cnt[CNT_EV_TIMER]++;
-      on_timer(D, x, node);
+    if (pick != CLS_TESTER) {
+      x.cnt[pick == CLS_MSG ? CNT_EV_MSG : CNT_EV_TIMER]++;
+      node_event(D, x, pick == CLS_MSG, node, x.mslot, (uint32_t)key & 0x3FFFFFFFu);
     } else {
       x.cnt[CNT_EV_TESTER]++;
       tester(D, x);
@@ -1337,6 +1411,10 @@ __global__ void __launch_bounds__(256, MR_WAVES_PER_EU) step_kernel(Dev D, uint3
   CS(CS_NOW) = x.now; CS(CS_EVENTS) = x.events; CS(CS_MSGS) = x.msgs_sent;
   CS(CS_INFLIGHT) = x.inflight; CS(CS_TRACEN) = x.trace_n; CS(CS_MSLOT) = x.mslot;
   CS(CS_NETMODE) = x.netmode; CS(CS_TCTR) = x.t_ctr;
+  CS(CS_CONN) = x.conn; CS(CS_ALIVE) = x.alive;
+#pragma unroll
+  for (uint32_t d = 0; d < MR_MAX_NODES; d++)
+    if (d < D.n) ND(NF_TIMER, d) = x.timer[d];
   C64(C64_FREE) = x.free_mask; C64(C64_DIGEST) = x.digest; C64(C64_MMIN) = x.mmin;
 #pragma unroll
   for (uint32_t k = 0; k < CNT__N; k++) CS(CS_CNT + k) = x.cnt[k];
@@ -1356,7 +1434,7 @@ __global__ void __launch_bounds__(256) reset_kernel(Dev D) {
   C64(C64_MMIN) = ~0ull;
   for (uint32_t d = 0; d < D.n; d++) {
     for (uint32_t f = 0; f < NF__N; f++) ND(f, d) = 0;
-    ND(NF_FLAGS, d) = 15u << 4;  // follower, down, disconnected, voted none
+    ND(NF_FLAGS, d) = 15u << 4;  // follower, voted none (down, disconnected: CS_ALIVE/CS_CONN = 0)
     ND(NF_TIMER, d) = INF_T;
     ND(NF_SLEN, d) = 1;
     NSV(d) = 0;
