@@ -26,6 +26,7 @@ def build_hip(force=False, verbose=False):
     srcs = sorted(glob.glob(os.path.join(HERE, "csrc", "*.hip")) +
                   glob.glob(os.path.join(HERE, "csrc", "*.cpp")))
     deps = srcs + glob.glob(os.path.join(HERE, "csrc", "*.h")) + \
+        glob.glob(os.path.join(HERE, "csrc", "*.inc")) + \
         [os.path.join(ROOT, "include", "madraft_sim.h")]
     if not force and not _stale(LIB, deps):
         return LIB

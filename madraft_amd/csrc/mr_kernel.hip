@@ -495,30 +495,6 @@ DI void node_event(const Dev& D, X& x, bool is_msg, uint32_t tnode, uint32_t slo
 }
 
 // ---------------------------------------------------------------- tester API (tester.rs)
-struct T {  // the tester coroutine frame, in registers during a tester event
-  uint32_t pc, res, helper;
-  uint32_t l[T_NL];
-  uint32_t h[T_NH];
-  uint64_t hv;
-};
-
-DI uint32_t t_draw(const Dev& D, X& x, uint32_t& w1) {
-  uint32_t w0;
-  philox(D, x, x.t_ctr++, 0, ST_TESTER, w0, w1);
-  return w0;
-}
-DI uint32_t t_range(const Dev& D, X& x, uint32_t lo, uint32_t hi) {
-  uint32_t w1, w0 = t_draw(D, x, w1);
-  return u_range(w0, lo, hi);
-}
-DI bool t_bool(const Dev& D, X& x, uint32_t p_q32) {
-  uint32_t w1;
-  return t_draw(D, x, w1) < p_q32;
-}
-DI uint64_t t_entry(const Dev& D, X& x) {  // tests.rs:943-951 gen_entry
-  uint32_t w1, w0 = t_draw(D, x, w1);
-  return ((uint64_t)w1 << 32) | w0;
-}
 DI void t_set_unrel(X& x, bool u) { x.netmode = (x.netmode & ~1u) | (u ? 1u : 0u); }
 DI bool t_started(const Dev& D, X& x, uint32_t i) { return bit(x.alive, i); }
 DI bool t_connected(const Dev& D, X& x, uint32_t i) { return bit(x.conn, i); }
@@ -606,704 +582,10 @@ DI void t_end(const Dev& D, X& x) {  // tester.rs:339-358
   rec_simple(D, x, 3, MR_PASS);
 }
 
-// ---- multi-event tester calls: step() returns true when done, false after
-// scheduling a sleep or failing. Frame: t.h[0..4], t.hv; result in t.res / t.hv.
-
-// check_one_leader, tester.rs:64-92. h0 iteration, h4 phase
-DI void col_init(T& t) { t.h[0] = 0; t.h[4] = 1; }
-DI bool col_step(const Dev& D, X& x, T& t) {
-  for (;;) {
-    if (t.h[4] == 1) {
-      if (t.h[0] >= 10) { fail(D, x, MR_FAIL_ONE_LEADER_NONE); return false; }
-      t_sleep(x, t_range(D, x, 450000u, 550000u));
-      t.h[4] = 2;
-      return false;
-    }
-    uint32_t best_term = 0, best = NONE, terms_seen = 0;
-    for (uint32_t i = 0; i < D.n; i++) {
-      if (!bit(x.conn, i)) continue;
-      if (!bit(x.alive, i)) { fail(D, x, MR_FAIL_UNWRAP_NONE); return false; }
-      if (D.null_raft || f_role(ND(NF_FLAGS, i)) != R_L) continue;
-      uint32_t ti = ND(NF_TERM, i);
-      for (uint32_t j = 0; j < i; j++) {  // >1 leaders in one term?
-        if (bit(x.conn, j) && f_role(ND(NF_FLAGS, j)) == R_L && ND(NF_TERM, j) == ti) {
-          fail(D, x, MR_FAIL_MULTI_LEADER_TERM);
-          return false;
-        }
-      }
-      terms_seen++;
-      if (best == NONE || ti > best_term) { best_term = ti; best = i; }
-    }
-    if (terms_seen) { t.res = best; return true; }
-    t.h[0]++;
-    t.h[4] = 1;
-  }
-}
-
-// one(cmd, expected, retry), tester.rs:216-262.
-// h0 t0, h1 starts, h2 index, h3 t1, h4 phase | expected << 8 | retry << 16; hv cmd
-DI void one_init(const Dev& D, X& x, T& t, uint64_t cmd, uint32_t expected, bool retry) {
-  t.hv = cmd;
-  t.h[0] = x.now;
-  t.h[1] = 0;
-  t.h[4] = 1u | (expected << 8) | (retry ? 1u << 16 : 0u);
-}
-DI bool one_step(const Dev& D, X& x, T& t) {
-  uint32_t expected = (t.h[4] >> 8) & 255u;
-  bool retry = (t.h[4] >> 16) & 1u;
-  for (;;) {
-    if ((t.h[4] & 255u) == 1) {
-      if (!(x.now - t.h[0] < 10000000u)) { fail(D, x, MR_FAIL_ONE_NO_AGREEMENT); return false; }
-      uint32_t starts = t.h[1], index = 0, term;
-      bool have = false;
-      for (uint32_t k = 0; k < D.n; k++) {
-        starts = (starts + 1) % D.n;
-        if (!bit(x.conn, starts) || !bit(x.alive, starts)) continue;
-        if (t_start(D, x, starts, t.hv, index, term)) { have = true; break; }
-        if (x.code != RUN) return false;
-      }
-      t.h[1] = starts;
-      if (!have) { t_sleep(x, 50000); return false; }
-      t.h[2] = index;
-      t.h[3] = x.now;
-      t.h[4] = (t.h[4] & ~255u) | 2u;
-    }
-    if (!(x.now - t.h[3] < 2000000u)) {
-      if (!retry) { fail(D, x, MR_FAIL_ONE_NO_AGREEMENT); return false; }
-      t.h[4] = (t.h[4] & ~255u) | 1u;
-      continue;
-    }
-    uint64_t v;
-    uint32_t cnt = n_committed(D, x, t.h[2], v);
-    if (cnt > 0 && cnt >= expected && v == t.hv) { t.res = t.h[2]; return true; }
-    t_sleep(x, 20000);
-    return false;
-  }
-}
-
-// wait(index, n, start_term), tester.rs:175-201.
-// h0 to, h1 iteration, h2 index, h3 start term, h4 phase | n << 8 | has_st << 16
-// result: t.res = Some?, t.hv = value
-DI void wait_init(T& t, uint32_t index, uint32_t nn, bool has_st, uint32_t st) {
-  t.h[0] = 10000; t.h[1] = 0; t.h[2] = index; t.h[3] = st;
-  t.h[4] = 1u | (nn << 8) | (has_st ? 1u << 16 : 0u);
-}
-DI bool wait_step(const Dev& D, X& x, T& t) {
-  uint32_t nn = (t.h[4] >> 8) & 255u;
-  uint64_t v;
-  if ((t.h[4] & 255u) == 2) {
-    if ((t.h[4] >> 16) & 1u) {
-      for (uint32_t i = 0; i < D.n; i++)
-        if (bit(x.alive, i) && ND(NF_TERM, i) > t.h[3]) { t.res = 0; return true; }
-    }
-    t.h[1]++;
-    t.h[4] = (t.h[4] & ~255u) | 1u;
-  }
-  uint32_t cnt = n_committed(D, x, t.h[2], v);
-  if (t.h[1] < 30 && cnt < nn) {
-    t_sleep(x, t.h[0]);
-    if (t.h[0] < 1000000u) t.h[0] *= 2;
-    t.h[4] = (t.h[4] & ~255u) | 2u;
-    return false;
-  }
-  if (cnt < nn) { fail(D, x, MR_FAIL_WAIT_TOO_FEW); return false; }
-  t.res = cnt > 0 ? 1u : 0u;
-  t.hv = v;
-  return true;
-}
-
-// ---- scenario state machines. Each test body (tests.rs) is split at its
-// suspension points into numbered states; a state ends by sleeping (SLEEP_TO),
-// by starting a multi-event tester call (ONE_TO / COL_TO / WAIT_TO) that the
-// dispatcher in tester() runs before resuming at the given state, by jumping
-// to another state (GO), or with the verdict. The dispatch loop over a switch
-// keeps the control flow reducible (protothread-style resumption into the
-// middle of loops made the AMDGPU structurizer blow up register pressure).
-// Persistent locals live in t.l[].
-enum : uint32_t { H_NONE = 0, H_ONE, H_COL, H_WAIT };
-#define CK() do { if (x.code != RUN) return; } while (0)
-#define GO(s) { t.pc = (s); continue; }
-#define SLEEP_TO(us, s) { t_sleep(x, (us)); t.pc = (s); return; }
-#define ONE_TO(cmd, e, r, s) \
-  { one_init(D, x, t, (cmd), (e), (r)); t.helper = H_ONE; t.pc = (s); return; }
-#define COL_TO(s) { col_init(t); t.helper = H_COL; t.pc = (s); return; }
-#define WAIT_TO(idx, nn, has, st, s) \
-  { wait_init(t, (idx), (nn), (has), (st)); t.helper = H_WAIT; t.pc = (s); return; }
-#define END() { t_end(D, x); return; }
-#define BAD() default: fail(D, x, MR_FAIL_SIM_BAD_PROGRAM); return;
+DI uint32_t nd_role(const Dev& D, X& x, uint32_t i) { return f_role(ND(NF_FLAGS, i)); }
+DI uint32_t nd_term(const Dev& D, X& x, uint32_t i) { return ND(NF_TERM, i); }
 #define TV(k) C64(C64_TV + (k))
-
-DI void scn_initial_election(const Dev& D, X& x, T& t) {  // tests.rs:20-46
-  for (;;) switch (t.pc) {
-    case 0: t_new(D, x, false); COL_TO(1)
-    case 1: SLEEP_TO(50000, 2)
-    case 2: t_check_terms(D, x); CK(); SLEEP_TO(2 * ELECTION_US, 3)
-    case 3: t_check_terms(D, x); CK(); COL_TO(4)  // term1 != term2 only warns
-    case 4: END()
-    BAD()
-  }
-}
-
-DI void scn_reelection(const Dev& D, X& x, T& t) {  // tests.rs:48-78
-  const uint32_t n = D.n;
-  uint32_t& l1 = t.l[0];
-  uint32_t& l2 = t.l[1];
-  for (;;) switch (t.pc) {
-    case 0: t_new(D, x, false); COL_TO(1)
-    case 1: l1 = t.res; t_conn(D, x, l1, 0); COL_TO(2)
-    case 2: t_conn(D, x, l1, 1); COL_TO(3)
-    case 3:
-      l2 = t.res;
-      t_conn(D, x, l2, 0);
-      t_conn(D, x, (l2 + 1) % n, 0);
-      SLEEP_TO(2 * ELECTION_US, 4)
-    case 4: t_check_no_leader(D, x); CK(); t_conn(D, x, (l2 + 1) % n, 1); COL_TO(5)
-    case 5: t_conn(D, x, l2, 1); COL_TO(6)
-    case 6: END()
-    BAD()
-  }
-}
-
-DI void scn_many_election(const Dev& D, X& x, T& t) {  // tests.rs:80-112
-  const uint32_t n = D.n;
-  uint32_t& it = t.l[0];
-  uint32_t& i1 = t.l[1];
-  uint32_t& i2 = t.l[2];
-  uint32_t& i3 = t.l[3];
-  for (;;) switch (t.pc) {
-    case 0: t_new(D, x, false); COL_TO(1)
-    case 1: it = 0; GO(2)
-    case 2:
-      if (it >= D.iters) COL_TO(4)
-      i1 = t_range(D, x, 0, n); i2 = t_range(D, x, 0, n); i3 = t_range(D, x, 0, n);
-      t_conn(D, x, i1, 0); t_conn(D, x, i2, 0); t_conn(D, x, i3, 0);
-      COL_TO(3)
-    case 3:
-      t_conn(D, x, i1, 1); t_conn(D, x, i2, 1); t_conn(D, x, i3, 1);
-      it++;
-      GO(2)
-    case 4: END()
-    BAD()
-  }
-}
-
-DI void scn_basic_agree(const Dev& D, X& x, T& t) {  // tests.rs:114-130
-  uint32_t& index = t.l[0];
-  for (;;) switch (t.pc) {
-    case 0: t_new(D, x, false); index = 1; GO(1)
-    case 1: {
-      if (index > 3) END()
-      uint64_t v;
-      if (n_committed(D, x, index, v) != 0) { fail(D, x, MR_FAIL_BASIC_PRECOMMIT); return; }
-      ONE_TO((uint64_t)index * 100, D.n, false, 2)
-    }
-    case 2:
-      if (t.res != index) { fail(D, x, MR_FAIL_BASIC_INDEX); return; }
-      index++;
-      GO(1)
-    BAD()
-  }
-}
-
-DI void scn_fail_agree(const Dev& D, X& x, T& t) {  // tests.rs:132-161
-  const uint32_t n = D.n;
-  uint32_t& leader = t.l[0];
-  for (;;) switch (t.pc) {
-    case 0: t_new(D, x, false); ONE_TO(101, n, false, 1)
-    case 1: COL_TO(2)
-    case 2: leader = t.res; t_conn(D, x, (leader + 1) % n, 0); ONE_TO(102, n - 1, false, 3)
-    case 3: ONE_TO(103, n - 1, false, 4)
-    case 4: SLEEP_TO(ELECTION_US, 5)
-    case 5: ONE_TO(104, n - 1, false, 6)
-    case 6: ONE_TO(105, n - 1, false, 7)
-    case 7: t_conn(D, x, (leader + 1) % n, 1); ONE_TO(106, n, true, 8)
-    case 8: SLEEP_TO(ELECTION_US, 9)
-    case 9: ONE_TO(107, n, true, 10)
-    case 10: END()
-    BAD()
-  }
-}
-
-DI void scn_fail_no_agree(const Dev& D, X& x, T& t) {  // tests.rs:163-209
-  const uint32_t n = D.n;
-  uint32_t& leader = t.l[0];
-  uint32_t& index = t.l[1];
-  for (;;) switch (t.pc) {
-    case 0: t_new(D, x, false); ONE_TO(10, n, false, 1)
-    case 1: COL_TO(2)
-    case 2: {
-      leader = t.res;
-      t_conn(D, x, (leader + 1) % n, 0);
-      t_conn(D, x, (leader + 2) % n, 0);
-      t_conn(D, x, (leader + 3) % n, 0);
-      uint32_t term;
-      bool ok = t_start(D, x, leader, 20, index, term);
-      CK();
-      if (!ok) { fail(D, x, MR_FAIL_LEADER_REJECTED); return; }
-      if (index != 2) { fail(D, x, MR_FAIL_EXPECTED_INDEX2); return; }
-      SLEEP_TO(2 * ELECTION_US, 3)
-    }
-    case 3: {
-      uint64_t v;
-      if (n_committed(D, x, index, v) != 0) { fail(D, x, MR_FAIL_NO_MAJORITY_COMMIT); return; }
-      t_conn(D, x, (leader + 1) % n, 1);
-      t_conn(D, x, (leader + 2) % n, 1);
-      t_conn(D, x, (leader + 3) % n, 1);
-      COL_TO(4)
-    }
-    case 4: {
-      uint32_t idx2, term;
-      bool ok = t_start(D, x, t.res, 30, idx2, term);
-      CK();
-      if (!ok) { fail(D, x, MR_FAIL_LEADER_REJECTED); return; }
-      if (idx2 < 2 || idx2 > 3) { fail(D, x, MR_FAIL_UNEXPECTED_INDEX); return; }
-      ONE_TO(1000, n, true, 5)
-    }
-    case 5: END()
-    BAD()
-  }
-}
-
-// (0..servers).any(|j| t.term(j) != term) with unwrap() semantics
-DI bool any_term_changed(const Dev& D, X& x, uint32_t term) {
-  for (uint32_t j = 0; j < D.n; j++) {
-    uint32_t tj = t_term(D, x, j);
-    if (x.code != RUN) return false;
-    if (tj != term) return true;
-  }
-  return false;
-}
-
-DI void scn_concurrent_starts(const Dev& D, X& x, T& t) {  // tests.rs:211-275
-  const uint32_t n = D.n;
-  uint32_t& tried = t.l[0];
-  uint32_t& term = t.l[1];
-  uint32_t& ni = t.l[2];  // idxes in TV(0..5)
-  uint32_t& q = t.l[3];
-  uint32_t& nc = t.l[4];  // cmds in TV(8..13)
-  for (;;) switch (t.pc) {
-    case 0: t_new(D, x, false); tried = 0; GO(1)
-    case 1:
-      if (tried >= 5) { fail(D, x, MR_FAIL_TERM_CHANGED); return; }  // assert!(success)
-      if (tried > 0) SLEEP_TO(3000000, 2)
-      GO(2)
-    case 2: COL_TO(3)
-    case 3: {
-      uint32_t leader = t.res, idx, st;
-      bool ok = t_start(D, x, leader, 1, idx, term);
-      CK();
-      if (!ok) { tried++; GO(1) }
-      ni = 0;
-      for (uint32_t ii = 0; ii < 5; ii++) {
-        bool ok2 = t_start(D, x, leader, 100 + ii, idx, st);
-        CK();
-        if (ok2 && st == term) { TV(ni) = idx; ni++; }
-      }
-      bool ch = any_term_changed(D, x, term);
-      CK();
-      if (ch) { tried++; GO(1) }
-      nc = 0;
-      q = 0;
-      GO(4)
-    }
-    case 4:
-      if (q >= ni) GO(6)
-      WAIT_TO((uint32_t)TV(q), n, true, term, 5)
-    case 5:
-      if (t.res) { TV(8 + nc) = t.hv; nc++; }
-      q++;
-      GO(4)
-    case 6:
-      for (uint32_t ii = 0; ii < 5; ii++) {
-        bool ok = false;
-        for (uint32_t k = 0; k < nc; k++)
-          if (TV(8 + k) == 100 + ii) ok = true;
-        if (!ok) { fail(D, x, MR_FAIL_CMD_MISSING); return; }
-      }
-      END()
-    BAD()
-  }
-}
-
-DI void scn_rejoin(const Dev& D, X& x, T& t) {  // tests.rs:277-313
-  const uint32_t n = D.n;
-  uint32_t& l1 = t.l[0];
-  uint32_t& l2 = t.l[1];
-  for (;;) switch (t.pc) {
-    case 0: t_new(D, x, false); ONE_TO(101, n, true, 1)
-    case 1: COL_TO(2)
-    case 2:
-      l1 = t.res;
-      t_conn(D, x, l1, 0);
-      t_start(D, x, l1, 102); CK();
-      t_start(D, x, l1, 103); CK();
-      t_start(D, x, l1, 104); CK();
-      ONE_TO(103, 2, true, 3)
-    case 3: COL_TO(4)
-    case 4: l2 = t.res; t_conn(D, x, l2, 0); t_conn(D, x, l1, 1); ONE_TO(104, 2, true, 5)
-    case 5: t_conn(D, x, l2, 1); ONE_TO(105, n, true, 6)
-    case 6: END()
-    BAD()
-  }
-}
-
-DI void scn_backup(const Dev& D, X& x, T& t) {  // tests.rs:315-386
-  const uint32_t n = D.n;
-  uint32_t& l1 = t.l[0];
-  uint32_t& l2 = t.l[1];
-  uint32_t& other = t.l[2];
-  uint32_t& i = t.l[3];
-  for (;;) switch (t.pc) {
-    case 0: t_new(D, x, false); ONE_TO(t_entry(D, x), n, true, 1)
-    case 1: COL_TO(2)
-    case 2:
-      l1 = t.res;
-      t_conn(D, x, (l1 + 2) % n, 0); t_conn(D, x, (l1 + 3) % n, 0); t_conn(D, x, (l1 + 4) % n, 0);
-      for (uint32_t k = 0; k < 50; k++) {
-        uint64_t e = t_entry(D, x);
-        t_start(D, x, l1, e); CK();
-      }
-      SLEEP_TO(ELECTION_US / 2, 3)
-    case 3:
-      t_conn(D, x, (l1 + 0) % n, 0); t_conn(D, x, (l1 + 1) % n, 0);
-      t_conn(D, x, (l1 + 2) % n, 1); t_conn(D, x, (l1 + 3) % n, 1); t_conn(D, x, (l1 + 4) % n, 1);
-      i = 0;
-      GO(4)
-    case 4:
-      if (i >= 50) COL_TO(6)
-      ONE_TO(t_entry(D, x), 3, true, 5)
-    case 5: i++; GO(4)
-    case 6:
-      l2 = t.res;
-      other = (l1 + 2) % n;
-      if (l2 == other) other = (l2 + 1) % n;
-      t_conn(D, x, other, 0);
-      for (uint32_t k = 0; k < 50; k++) {
-        uint64_t e = t_entry(D, x);
-        t_start(D, x, l2, e); CK();
-      }
-      SLEEP_TO(ELECTION_US / 2, 7)
-    case 7:
-      for (uint32_t k = 0; k < n; k++) t_conn(D, x, k, 0);
-      t_conn(D, x, (l1 + 0) % n, 1); t_conn(D, x, (l1 + 1) % n, 1); t_conn(D, x, other, 1);
-      i = 0;
-      GO(8)
-    case 8:
-      if (i >= 50) {
-        for (uint32_t k = 0; k < n; k++) t_conn(D, x, k, 1);
-        ONE_TO(t_entry(D, x), n, true, 10)
-      }
-      ONE_TO(t_entry(D, x), 3, true, 9)
-    case 9: i++; GO(8)
-    case 10: END()
-    BAD()
-  }
-}
-
-DI void scn_count(const Dev& D, X& x, T& t) {  // tests.rs:388-479
-  const uint32_t n = D.n;
-  uint32_t& total1 = t.l[0];
-  uint32_t& total2 = t.l[1];
-  uint32_t& tried = t.l[2];
-  uint32_t& starti = t.l[3];
-  uint32_t& term = t.l[4];
-  uint32_t& i = t.l[5];
-  for (;;) switch (t.pc) {
-    case 0: t_new(D, x, false); COL_TO(1)
-    case 1:
-      total1 = x.msgs_sent / 2;
-      if (total1 < 1 || total1 > 30) { fail(D, x, MR_FAIL_RPC_INITIAL); return; }
-      total2 = 0;
-      tried = 0;
-      GO(2)
-    case 2:
-      if (tried >= 5) { fail(D, x, MR_FAIL_TERM_CHANGED); return; }
-      if (tried > 0) SLEEP_TO(3000000, 3)
-      GO(3)
-    case 3: COL_TO(4)
-    case 4: {
-      total1 = x.msgs_sent / 2;
-      uint32_t leader = t.res, idx, st;
-      bool ok = t_start(D, x, leader, 1, starti, term);
-      CK();
-      if (!ok) { tried++; GO(2) }
-      bool outer = false;
-      for (uint32_t k = 1; k < 10 + 2; k++) {
-        uint64_t xv = t_entry(D, x);  // random.gen::<u64>()
-        TV(k - 1) = xv;
-        bool ok2 = t_start(D, x, leader, xv, idx, st);
-        CK();
-        if (!ok2 || st != term) { outer = true; break; }
-        if (starti + k != idx) { fail(D, x, MR_FAIL_START_FAILED); return; }
-      }
-      if (outer) { tried++; GO(2) }
-      i = 1;
-      GO(5)
-    }
-    case 5:
-      if (i > 10) GO(7)
-      WAIT_TO(starti + i, n, true, term, 6)
-    case 6:
-      if (t.res && t.hv != TV(i - 1)) { fail(D, x, MR_FAIL_WRONG_VALUE); return; }
-      i++;
-      GO(5)
-    case 7: {
-      bool ch = any_term_changed(D, x, term);
-      CK();
-      if (ch) { tried++; GO(2) }
-      total2 = x.msgs_sent / 2;
-      if (total2 - total1 > (10 + 1 + 3) * 3) { fail(D, x, MR_FAIL_RPC_TOO_MANY); return; }
-      SLEEP_TO(ELECTION_US, 8)
-    }
-    case 8:
-      if (x.msgs_sent / 2 - total2 > 3 * 20) { fail(D, x, MR_FAIL_RPC_IDLE); return; }
-      END()
-    BAD()
-  }
-}
-
-DI void scn_persist1(const Dev& D, X& x, T& t) {  // tests.rs:481-526
-  const uint32_t n = D.n;
-  uint32_t& l = t.l[0];
-  for (;;) switch (t.pc) {
-    case 0: t_new(D, x, false); ONE_TO(11, n, true, 1)
-    case 1:
-      for (uint32_t i = 0; i < n; i++) t_start1(D, x, i);
-      for (uint32_t i = 0; i < n; i++) { t_conn(D, x, i, 0); t_conn(D, x, i, 1); }
-      ONE_TO(12, n, true, 2)
-    case 2: COL_TO(3)
-    case 3:
-      l = t.res;
-      t_conn(D, x, l, 0); t_start1(D, x, l); t_conn(D, x, l, 1);
-      ONE_TO(13, n, true, 4)
-    case 4: COL_TO(5)
-    case 5: l = t.res; t_conn(D, x, l, 0); ONE_TO(14, n - 1, true, 6)
-    case 6: t_start1(D, x, l); t_conn(D, x, l, 1); WAIT_TO(4, n, false, 0, 7)
-    case 7: COL_TO(8)
-    case 8: l = (t.res + 1) % n; t_conn(D, x, l, 0); ONE_TO(15, n - 1, true, 9)
-    case 9: t_start1(D, x, l); t_conn(D, x, l, 1); ONE_TO(16, n, true, 10)
-    case 10: END()
-    BAD()
-  }
-}
-
-DI void scn_persist2(const Dev& D, X& x, T& t) {  // tests.rs:528-572
-  const uint32_t n = D.n;
-  uint32_t& index = t.l[0];
-  uint32_t& k = t.l[1];
-  uint32_t& l1 = t.l[2];
-  for (;;) switch (t.pc) {
-    case 0: t_new(D, x, false); index = 1; k = 0; GO(1)
-    case 1:
-      if (k >= 5) ONE_TO(1000, n, true, 7)
-      ONE_TO(10 + index, n, true, 2)
-    case 2: index++; COL_TO(3)
-    case 3:
-      l1 = t.res;
-      t_conn(D, x, (l1 + 1) % n, 0); t_conn(D, x, (l1 + 2) % n, 0);
-      ONE_TO(10 + index, n - 2, true, 4)
-    case 4:
-      index++;
-      t_conn(D, x, (l1 + 0) % n, 0); t_conn(D, x, (l1 + 3) % n, 0); t_conn(D, x, (l1 + 4) % n, 0);
-      t_start1(D, x, (l1 + 1) % n); t_start1(D, x, (l1 + 2) % n);
-      t_conn(D, x, (l1 + 1) % n, 1); t_conn(D, x, (l1 + 2) % n, 1);
-      SLEEP_TO(ELECTION_US, 5)
-    case 5:
-      t_start1(D, x, (l1 + 3) % n); t_conn(D, x, (l1 + 3) % n, 1);
-      ONE_TO(10 + index, n - 2, true, 6)
-    case 6:
-      index++;
-      t_conn(D, x, (l1 + 4) % n, 1); t_conn(D, x, (l1 + 0) % n, 1);
-      k++;
-      GO(1)
-    case 7: END()
-    BAD()
-  }
-}
-
-DI void scn_persist3(const Dev& D, X& x, T& t) {  // tests.rs:574-602
-  const uint32_t n = D.n;
-  uint32_t& leader = t.l[0];
-  for (;;) switch (t.pc) {
-    case 0: t_new(D, x, false); ONE_TO(101, 3, true, 1)
-    case 1: COL_TO(2)
-    case 2: leader = t.res; t_conn(D, x, (leader + 2) % n, 0); ONE_TO(102, 2, true, 3)
-    case 3:
-      t_crash1(D, x, (leader + 0) % n); t_crash1(D, x, (leader + 1) % n);
-      t_conn(D, x, (leader + 2) % n, 1);
-      t_start1(D, x, (leader + 0) % n); t_conn(D, x, (leader + 0) % n, 1);
-      ONE_TO(103, 2, true, 4)
-    case 4:
-      t_start1(D, x, (leader + 1) % n); t_conn(D, x, (leader + 1) % n, 1);
-      ONE_TO(104, n, true, 5)
-    case 5: END()
-    BAD()
-  }
-}
-
-DI uint32_t fig8_delay(const Dev& D, X& x) {  // tests.rs:631-635 / 711-715
-  if (t_bool(D, x, LOSS_Q32)) return t_range(D, x, 0, ELECTION_US / 2);
-  return t_range(D, x, 0, 13000);
-}
-
-// figure_8_2c (tests.rs:612-660); with `unreliable` the config-3 literal variant
-DI void scn_figure_8(const Dev& D, X& x, T& t, bool unreliable) {
-  const uint32_t n = D.n;
-  uint32_t& nup = t.l[0];
-  uint32_t& it = t.l[1];
-  uint32_t& leader = t.l[2];
-  for (;;) switch (t.pc) {
-    case 0:
-      t_new(D, x, false);
-      if (unreliable) t_set_unrel(x, true);
-      ONE_TO(t_entry(D, x), 1, true, 1)
-    case 1: nup = n; it = 0; GO(2)
-    case 2:
-      if (it >= D.iters) {
-        for (uint32_t i = 0; i < n; i++)
-          if (!t_started(D, x, i)) t_start1(D, x, i);
-        ONE_TO(t_entry(D, x), n, true, 4)
-      }
-      leader = NONE;
-      for (uint32_t i = 0; i < n; i++) {
-        if (!t_started(D, x, i)) continue;
-        uint64_t e = t_entry(D, x);
-        bool ok = t_start(D, x, i, e);
-        CK();
-        if (ok) leader = i;
-      }
-      SLEEP_TO(fig8_delay(D, x), 3)
-    case 3:
-      if (leader != NONE) { t_crash1(D, x, leader); nup--; }
-      if (nup < 3) {
-        uint32_t s = t_range(D, x, 0, n);
-        if (!t_started(D, x, s)) { t_start1(D, x, s); nup++; }
-      }
-      it++;
-      GO(2)
-    case 4: END()
-    BAD()
-  }
-}
-
-DI void scn_figure_8_unreliable(const Dev& D, X& x, T& t) {  // tests.rs:688-741
-  const uint32_t n = D.n;
-  uint32_t& nup = t.l[0];
-  uint32_t& it = t.l[1];
-  uint32_t& leader = t.l[2];
-  for (;;) switch (t.pc) {
-    case 0:
-      t_new(D, x, false);
-      t_set_unrel(x, true);
-      ONE_TO(t_entry(D, x), 1, true, 1)
-    case 1: nup = n; it = 0; GO(2)
-    case 2:
-      if (it >= D.iters) {
-        for (uint32_t i = 0; i < n; i++) t_conn(D, x, i, 1);
-        ONE_TO(t_entry(D, x), n, true, 4)
-      }
-      leader = NONE;
-      for (uint32_t i = 0; i < n; i++) {
-        uint64_t e = t_entry(D, x);
-        bool ok = t_start(D, x, i, e);
-        CK();
-        if (ok && t_connected(D, x, i)) leader = i;
-      }
-      SLEEP_TO(fig8_delay(D, x), 3)
-    case 3:
-      if (leader != NONE && t_range(D, x, 0, 1000) < ELECTION_US / 1000 / 2) {
-        t_conn(D, x, leader, 0);
-        nup--;
-      }
-      if (nup < 3) {
-        uint32_t s = t_range(D, x, 0, n);
-        if (!t_connected(D, x, s)) { t_conn(D, x, s, 1); nup++; }
-      }
-      it++;
-      GO(2)
-    case 4: END()
-    BAD()
-  }
-}
-
-DI void scn_snap_common(const Dev& D, X& x, T& t, bool disconnect, bool reliable, bool crash) {
-  // tests.rs:858-911
-  const uint32_t n = D.n;
-  uint32_t& leader1 = t.l[0];
-  uint32_t& i = t.l[1];
-  uint32_t& victim = t.l[2];
-  for (;;) switch (t.pc) {
-    case 0:
-      t_new(D, x, true);
-      t_set_unrel(x, !reliable);
-      ONE_TO(t_entry(D, x), n, true, 1)
-    case 1: COL_TO(2)
-    case 2: leader1 = t.res; i = 0; GO(3)
-    case 3:
-      if (i >= D.iters) END()
-      victim = (i % 3 == 1) ? leader1 : (leader1 + 1) % n;
-      if (disconnect) { t_conn(D, x, victim, 0); ONE_TO(t_entry(D, x), n - 1, true, 4) }
-      GO(4)
-    case 4:
-      if (crash) { t_crash1(D, x, victim); ONE_TO(t_entry(D, x), n - 1, true, 5) }
-      GO(5)
-    case 5: {
-      uint32_t sender = (i % 3 == 1) ? (leader1 + 1) % n : leader1;
-      for (uint32_t k = 0; k <= 10; k++) {  // send enough to get a snapshot
-        uint64_t e = t_entry(D, x);
-        t_start(D, x, sender, e);
-        CK();
-      }
-      ONE_TO(t_entry(D, x), n - 1, true, 6)
-    }
-    case 6:
-      if (t_log_size(D, x) >= 2000) { fail(D, x, MR_FAIL_LOG_SIZE); return; }
-      if (disconnect) { t_conn(D, x, victim, 1); ONE_TO(t_entry(D, x), n, true, 7) }
-      GO(9)
-    case 7: COL_TO(8)
-    case 8: leader1 = t.res; GO(9)
-    case 9:
-      if (crash) {
-        t_start1(D, x, victim);
-        t_conn(D, x, victim, 1);
-        ONE_TO(t_entry(D, x), n, true, 10)
-      }
-      GO(12)
-    case 10: COL_TO(11)
-    case 11: leader1 = t.res; GO(12)
-    case 12: i++; GO(3)
-    BAD()
-  }
-}
-
-DI void run_scenario(const Dev& D, X& x, T& t) {
-  switch (D.scenario) {
-    case MR_SCN_INITIAL_ELECTION_2A: scn_initial_election(D, x, t); break;
-    case MR_SCN_REELECTION_2A: scn_reelection(D, x, t); break;
-    case MR_SCN_MANY_ELECTION_2A: scn_many_election(D, x, t); break;
-    case MR_SCN_BASIC_AGREE_2B: scn_basic_agree(D, x, t); break;
-    case MR_SCN_FAIL_AGREE_2B: scn_fail_agree(D, x, t); break;
-    case MR_SCN_FAIL_NO_AGREE_2B: scn_fail_no_agree(D, x, t); break;
-    case MR_SCN_CONCURRENT_STARTS_2B: scn_concurrent_starts(D, x, t); break;
-    case MR_SCN_REJOIN_2B: scn_rejoin(D, x, t); break;
-    case MR_SCN_BACKUP_2B: scn_backup(D, x, t); break;
-    case MR_SCN_COUNT_2B: scn_count(D, x, t); break;
-    case MR_SCN_PERSIST1_2C: scn_persist1(D, x, t); break;
-    case MR_SCN_PERSIST2_2C: scn_persist2(D, x, t); break;
-    case MR_SCN_PERSIST3_2C: scn_persist3(D, x, t); break;
-    case MR_SCN_FIGURE_8_2C: scn_figure_8(D, x, t, false); break;
-    case MR_SCN_FIGURE_8_UNRELIABLE_CRASH: scn_figure_8(D, x, t, true); break;
-    case MR_SCN_FIGURE_8_UNRELIABLE_2C: scn_figure_8_unreliable(D, x, t); break;
-    case MR_SCN_SNAPSHOT_BASIC_2D: scn_snap_common(D, x, t, false, true, false); break;
-    case MR_SCN_SNAPSHOT_INSTALL_2D: scn_snap_common(D, x, t, true, true, false); break;
-    case MR_SCN_SNAPSHOT_INSTALL_UNRELIABLE_2D: scn_snap_common(D, x, t, true, false, false); break;
-    case MR_SCN_SNAPSHOT_INSTALL_CRASH_2D: scn_snap_common(D, x, t, false, true, true); break;
-    case MR_SCN_SNAPSHOT_INSTALL_UNRELIABLE_CRASH_2D:
-      scn_snap_common(D, x, t, false, false, true);
-      break;
-    default: fail(D, x, MR_FAIL_SIM_BAD_PROGRAM); return;
-  }
-}
+#include "mr_tester.inc"
 
 // one tester event: resume the cluster's coroutine until it sleeps or ends
 DI void tester(const Dev& D, X& x) {
@@ -1391,15 +673,24 @@ __global__ void __launch_bounds__(256, MR_WAVES_PER_EU) step_kernel(Dev D, uint3
     const uint32_t nm = __popcll(__ballot(run && cls == CLS_MSG));
     const uint32_t nt = __popcll(__ballot(run && cls == CLS_TIMER));
     const uint32_t ns = __popcll(__ballot(run && cls == CLS_TESTER));
-    const uint32_t pick = (2 * ns >= nm + nt + ns) ? CLS_TESTER : (nm >= nt ? CLS_MSG : CLS_TIMER);
-    if (!run || cls != pick) continue;
+#ifndef MR_TESTER_NUM  // tester events run when >= NUM/DEN of the live lanes want them
+#define MR_TESTER_NUM 1
+#define MR_TESTER_DEN 3
+#endif
+#ifndef MR_MERGE_NODE  // message and timer events share one class (one node_event pass)
+#define MR_MERGE_NODE 1
+#endif
+    const bool tpick = MR_TESTER_DEN * ns >= MR_TESTER_NUM * (nm + nt + ns);
+    const uint32_t pick = tpick ? CLS_TESTER : (nm >= nt ? CLS_MSG : CLS_TIMER);
+    const bool mine = MR_MERGE_NODE ? (tpick ? cls == CLS_TESTER : cls != CLS_TESTER) : cls == pick;
+    if (!run || !mine) continue;
     x.now = (uint32_t)(key >> 32);
     need = true;
     x.events++;
     if (x.events > D.max_events) { fail(D, x, MR_FAIL_SIM_EVENT_LIMIT); continue; }
-    if (pick != CLS_TESTER) {
-      x.cnt[pick == CLS_MSG ? CNT_EV_MSG : CNT_EV_TIMER]++;
-      node_event(D, x, pick == CLS_MSG, node, x.mslot, (uint32_t)key & 0x3FFFFFFFu);
+    if (cls != CLS_TESTER) {
+      x.cnt[cls == CLS_MSG ? CNT_EV_MSG : CNT_EV_TIMER]++;
+      node_event(D, x, cls == CLS_MSG, node, x.mslot, (uint32_t)key & 0x3FFFFFFFu);
     } else {
       x.cnt[CNT_EV_TESTER]++;
       tester(D, x);
