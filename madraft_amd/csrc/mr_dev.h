@@ -55,6 +55,13 @@ enum : uint32_t { PF_NEXT, PF_MATCH, PF__N };
 enum : uint32_t { MF_HDR, MF_TERM, MF_A, MF_B, MF_C, MF__N };
 enum : uint32_t { M64_KEY, M64_V, M64__N };
 
+// one Raft log entry (raft.rs Log: term + command), 16 B so an entry moves as
+// one 128-bit access; message payloads (AppendEntries entries) use the same form
+struct alignas(16) LE {
+  uint32_t term, pad;
+  uint64_t val;
+};
+
 // ---- everything the kernels see (passed by value as a kernel argument)
 struct Dev {
   // config
@@ -68,14 +75,14 @@ struct Dev {
   uint32_t* pr32;
   uint32_t* ms32;
   uint64_t* ms64;
-  uint32_t* lterm;  // [C][n][log_cap]
-  uint64_t* lval;
-  uint32_t* pterm;  // [C][M][K]
-  uint64_t* pval;
+  LE* log;  // [C][n][log_cap] ring per node
+  LE* pay;  // [C][M][K] AppendEntries payload per message slot
   uint8_t* smask;   // [C][apply_cap]   tester storage (tester.rs:366-428)
   uint64_t* sval;
   mr_event* trace;  // [trace_clusters][trace_cap]
   uint32_t* remaining;  // clusters without verdict after a step launch
+  unsigned long long* prof;  // [PROF_SLOTS] wave-cycle profile (MR_PROF builds only)
 };
+constexpr uint32_t PROF_SLOTS = 64;
 
 }  // namespace mr

@@ -205,14 +205,13 @@ int mr_batch_create(const mr_cfg* cfg, mr_batch** out) {
   add(&D.pr32, (size_t)PF__N * n * n * C);
   add(&D.ms32, (size_t)MF__N * M * C);
   add(&D.ms64, (size_t)M64__N * M * C);
-  add(&D.lterm, C * n * cfg->log_cap);
-  add(&D.lval, C * n * cfg->log_cap);
-  add(&D.pterm, C * M * K);
-  add(&D.pval, C * M * K);
+  add(&D.log, C * n * cfg->log_cap);
+  add(&D.pay, C * M * K);
   add(&D.smask, C * cfg->apply_cap);
   add(&D.sval, C * cfg->apply_cap);
   add(&D.trace, (size_t)D.trace_clusters * D.trace_cap);
   add(&D.remaining, 1);
+  add(&D.prof, PROF_SLOTS);
   size_t total = 0;
   for (auto& it : items) total += (it.bytes + 255) & ~size_t(255);
 
@@ -234,6 +233,10 @@ int mr_batch_create(const mr_cfg* cfg, mr_batch** out) {
   for (auto& it : items) {
     *it.p = p;
     p += (it.bytes + 255) & ~size_t(255);
+  }
+  if (hipMemset(b->D.prof, 0, PROF_SLOTS * sizeof(unsigned long long)) != hipSuccess) {
+    mr_batch_destroy(b);
+    return set_err("hipMemset failed");
   }
   if (const char* s = std::getenv("MR_STEP_BUDGET")) b->budget = (uint32_t)std::atoi(s);
   if (b->budget == 0) b->budget = 2048;
@@ -367,6 +370,16 @@ void mr_batch_destroy(mr_batch* b) {
   if (!b) return;
   (void)hipSetDevice(b->cfg.device);
   if (b->stream) (void)hipStreamSynchronize(b->stream);
+#ifdef MR_PROF
+  if (b->base) {  // development profile: wave cycles per kernel section (mr_kernel.hip PROF_*)
+    unsigned long long h[PROF_SLOTS];
+    if (hipMemcpy(h, b->D.prof, sizeof h, hipMemcpyDeviceToHost) == hipSuccess) {
+      std::fprintf(stderr, "MRPROF");
+      for (uint32_t k = 0; k < PROF_SLOTS; k++) std::fprintf(stderr, " %llu", h[k]);
+      std::fprintf(stderr, "\n");
+    }
+  }
+#endif
   if (b->base) (void)hipFree(b->base);
   if (b->red) (void)hipFree(b->red);
   if (b->h_remaining) (void)hipHostFree(b->h_remaining);

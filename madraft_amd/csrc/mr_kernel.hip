@@ -40,7 +40,9 @@ struct X {
   uint32_t conn, alive;  // node bit masks: connected (net clog state), started (tester.rs:24-25)
   uint64_t free_mask, digest, mmin;
   uint32_t timer[MR_MAX_NODES];  // node timers (election / heartbeat deadline), INF_T = none
+#if !MR_CNT_MEM
   uint32_t cnt[CNT__N];
+#endif
 };
 
 // field accessors (32-bit element offsets, checked at batch creation)
@@ -51,8 +53,50 @@ struct X {
 #define PR(f, d, p) D.pr32[(((uint32_t)(f) * D.n + (d)) * D.n + (p)) * D.C + x.c]
 #define MS32(f, mi) D.ms32[(uint32_t)(f) * D.M * D.C + (mi)]
 #define MS64(f, mi) D.ms64[(uint32_t)(f) * D.M * D.C + (mi)]
+// message keys of the lane's cluster live in LDS during a launch: [slot][lane],
+// so a wave's 64 lanes read 64 consecutive u64 (conflict-free). Free slots hold
+// ~0, so the earliest-message scan is a branch-free min over all M slots.
+constexpr uint32_t STEP_BLOCK = 128;
+extern __shared__ uint64_t s_keys[];
+#define LK(s) s_keys[(s) * STEP_BLOCK + threadIdx.x]
+
+// Development profile (MR_PROF builds): the first active lane of a wave adds
+// the wave cycles since the previous mark to section k, so the sections
+// partition each wave's time; slot 32 + k counts the marks.
+enum : uint32_t {
+  P_TAIL, P_SEL, P_DECODE, P_LOAD, P_DROP, P_RVREQ, P_RVREP, P_AEREQ, P_AEREP, P_ISREQ, P_ISREP,
+  P_HB, P_ELECT, P_APPLY, P_SEND, P_STORE, P_TESTER, P_STEPDOWN, P_PRO, P_EPI, P__N
+};
+#ifdef MR_PROF
+__shared__ unsigned long long s_prof[STEP_BLOCK / 64][2 * P__N + 1];
+#define PROF(k)                                                            \
+  do {                                                                     \
+    unsigned long long t_ = wall_clock64();                                \
+    if (__lane_id() == (uint32_t)__builtin_ctzll(__ballot(1))) {           \
+      uint32_t w_ = threadIdx.x >> 6;                                      \
+      unsigned long long d_ = t_ - s_prof[w_][2 * P__N];                   \
+      if ((long long)d_ > 0) s_prof[w_][k] += d_;                          \
+      s_prof[w_][P__N + (k)] += 1;                                         \
+      s_prof[w_][2 * P__N] = t_;                                           \
+    }                                                                      \
+  } while (0)
+#else
+#define PROF(k) do {} while (0)
+#endif
 
 // ---------------------------------------------------------------- helpers
+// per-cluster statistics counters: in registers, or (MR_CNT_MEM) updated in
+// place with fire-and-forget atomics so they hold no registers
+#ifndef MR_CNT_MEM
+#define MR_CNT_MEM 0
+#endif
+#if MR_CNT_MEM
+#define CADD(k, v) __hip_atomic_fetch_add(&CS(CS_CNT + (k)), (uint32_t)(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+#define CMAX(k, v) __hip_atomic_fetch_max(&CS(CS_CNT + (k)), (uint32_t)(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+#else
+#define CADD(k, v) (x.cnt[k] += (v))
+#define CMAX(k, v) do { uint32_t v_ = (v); if (v_ > x.cnt[k]) x.cnt[k] = v_; } while (0)
+#endif
 // node flag word: role[0:2) voted[4:8) (15 = none) inc[8:16) votes[16:24)
 DI uint32_t f_role(uint32_t f) { return f & 3u; }
 DI uint32_t f_voted(uint32_t f) { return (f >> 4) & 15u; }
@@ -126,7 +170,7 @@ DI void store_node(const Dev& D, const X& x, uint32_t d, const NC& n) {
 DI uint32_t term_at(const Dev& D, const X& x, uint32_t d, const NC& n, uint32_t i) {
   if (i == 0) return 0;
   if (i == n.snap) return n.snapt;
-  return D.lterm[logi(D, x, d, i)];
+  return D.log[logi(D, x, d, i)].term;
 }
 
 DI uint32_t net_loss(const X& x) { return (x.netmode & 1u) ? LOSS_Q32 : 0u; }  // tester.rs:127-137
@@ -178,10 +222,9 @@ DI void reset_timer(const Dev& D, X& x, uint32_t d, NC& n) {  // raft.rs:260-263
 DI void rescan_min(const Dev& D, X& x) {
   uint64_t best = ~0ull;
   uint32_t bs = 0;
-  uint64_t occ = ~x.free_mask;
+#pragma unroll 8
   for (uint32_t s = 0; s < D.M; s++) {
-    if (!((occ >> s) & 1ull)) continue;
-    uint64_t k = MS64(M64_KEY, s * D.C + x.c);
+    uint64_t k = LK(s);
     if (k < best) { best = k; bs = s; }
   }
   x.mmin = best;
@@ -195,44 +238,29 @@ DI int net_send(const Dev& D, X& x, uint32_t src, NC& s, uint32_t dst, uint32_t 
                 uint32_t k) {
   uint32_t seq = x.msgs_sent++;
   uint32_t ctr = s.nctr++;
-  if (!bit(x.conn, src) || !bit(x.conn, dst)) { x.cnt[CNT_DROP_CLOG]++; return -1; }
+  if (!bit(x.conn, src) || !bit(x.conn, dst)) { CADD(CNT_DROP_CLOG, 1u); return -1; }
   uint32_t w0, w1;
   philox(D, x, ctr, src, ST_NET, w0, w1);
-  if (w0 < net_loss(x)) { x.cnt[CNT_DROP_LOSS]++; return -1; }
-  if (x.inflight >= D.M) { x.cnt[CNT_DROP_OVERFLOW]++; return -1; }
+  if (w0 < net_loss(x)) { CADD(CNT_DROP_LOSS, 1u); return -1; }
+  if (x.inflight >= D.M) { CADD(CNT_DROP_OVERFLOW, 1u); return -1; }
   if (seq >= (1u << 30)) { fail(D, x, MR_FAIL_SIM_CAPACITY); return -1; }
   uint32_t t = x.now + u_range(w1, 1000u, net_lat_hi(x));
   uint32_t slot = (uint32_t)__builtin_ctzll(x.free_mask);
   x.free_mask &= ~(1ull << slot);
   uint64_t key = ((uint64_t)t << 32) | seq;
   uint32_t mi = slot * D.C + x.c;
-  MS64(M64_KEY, mi) = key;
+  LK(slot) = key;
   MS32(MF_HDR, mi) = type | (src << 3) | (dst << 6) | (inc << 9) | (k << 17);
   MS32(MF_TERM, mi) = term; MS32(MF_A, mi) = a; MS32(MF_B, mi) = b; MS32(MF_C, mi) = c;
   if (type == M_IS_REQ) MS64(M64_V, mi) = v;
   x.inflight++;
-  if (x.inflight > x.cnt[CNT_MAX_INFLIGHT]) x.cnt[CNT_MAX_INFLIGHT] = x.inflight;
+  CMAX(CNT_MAX_INFLIGHT, x.inflight);
   if (key < x.mmin) { x.mmin = key; x.mslot = slot; }
   return (int)slot;
 }
 
 // ---------------------------------------------------------------- tester storage
-DI void push_and_check(const Dev& D, X& x, uint32_t i, uint32_t idx, uint64_t v) {
-  if (idx >= D.apply_cap) { fail(D, x, MR_FAIL_SIM_CAPACITY); return; }
-  x.cnt[CNT_APPLIES]++;
-  size_t si = (size_t)x.c * D.apply_cap + idx;
-  uint32_t m = D.smask[si];
-  if (m && D.sval[si] != v) { fail(D, x, MR_FAIL_APPLY_MISMATCH); return; }  // tester.rs:384
-  uint32_t len = ND(NF_SLEN, i);
-  if (idx > len) { fail(D, x, MR_FAIL_APPLY_OUT_OF_ORDER); return; }  // tester.rs:393
-  if (idx == len) {
-    D.sval[si] = v;
-    D.smask[si] = (uint8_t)(m | (1u << i));
-    ND(NF_SLEN, i) = len + 1;
-    if (idx > x.cnt[CNT_MAX_INDEX]) x.cnt[CNT_MAX_INDEX] = idx;
-  }
-}
-
+constexpr uint32_t AC = 4;  // entries per batch of independent loads in log walks
 DI void storage_snapshot(const Dev& D, X& x, uint32_t i, uint32_t idx) {  // tester.rs:399-402
   if (idx >= D.apply_cap) { fail(D, x, MR_FAIL_SIM_CAPACITY); return; }
   uint32_t nl = idx + 1, len = ND(NF_SLEN, i);
@@ -262,20 +290,51 @@ DI uint32_t n_committed(const Dev& D, X& x, uint32_t idx, uint64_t& v) {  // tes
 // changes and its applies, in ascending peer order.
 enum : uint32_t { SEND_NONE = 0, SEND_REPLY, SEND_APPEND, SEND_VOTE };
 
-DI void node_apply(const Dev& D, X& x, uint32_t me, NC& d) {  // tester.rs:302-325 applier
-  bool snapmode = (x.netmode >> 1) & 1u;
+// the tester's applier (tester.rs:302-325) with push_and_check
+// (tester.rs:366-396) inlined: committed entries are walked in batches of AC
+// whose loads (log entry, storage mask / value) are all issued before any is
+// used — entries have distinct indices, so a batch never reads what it writes.
+DI void node_apply(const Dev& D, X& x, uint32_t me, NC& d) {
+  const bool snapmode = (x.netmode >> 1) & 1u;
+  const size_t sb = (size_t)x.c * D.apply_cap;
+  uint32_t len = ND(NF_SLEN, me);
   while (d.applied < d.commit) {
-    uint32_t i = ++d.applied;
-    uint64_t v = D.lval[logi(D, x, me, i)];
-    push_and_check(D, x, me, i, v);
-    if (x.code != RUN) return;
-    if (snapmode && (i + 1) % 10u == 0 && i > d.snap) {
-      d.snapt = term_at(D, x, me, d, i);
-      d.snap = i;
-      NSV(me) = v;
-      x.cnt[CNT_SNAPSHOTS]++;
+    const uint32_t i0 = d.applied + 1;
+    LE e[AC];
+    uint32_t m[AC];
+    uint64_t sv[AC];
+#pragma unroll
+    for (uint32_t j = 0; j < AC; j++) {
+      const uint32_t i = i0 + j;
+      const bool ok = i <= d.commit && i < D.apply_cap;
+      e[j] = ok ? D.log[logi(D, x, me, i)] : LE{};
+      m[j] = ok ? D.smask[sb + i] : 0u;
+      sv[j] = ok ? D.sval[sb + i] : 0ull;
+    }
+#pragma unroll
+    for (uint32_t j = 0; j < AC; j++) {
+      const uint32_t i = i0 + j;
+      if (i > d.commit) break;
+      d.applied = i;
+      if (i >= D.apply_cap) { fail(D, x, MR_FAIL_SIM_CAPACITY); return; }
+      CADD(CNT_APPLIES, 1u);
+      if (m[j] && sv[j] != e[j].val) { fail(D, x, MR_FAIL_APPLY_MISMATCH); return; }  // tester.rs:384
+      if (i > len) { fail(D, x, MR_FAIL_APPLY_OUT_OF_ORDER); return; }  // tester.rs:393
+      if (i == len) {
+        D.sval[sb + i] = e[j].val;
+        D.smask[sb + i] = (uint8_t)(m[j] | (1u << me));
+        len++;
+        CMAX(CNT_MAX_INDEX, i);
+      }
+      if (snapmode && (i + 1) % 10u == 0 && i > d.snap) {  // 2D: service snapshots every 10
+        d.snapt = e[j].term;
+        d.snap = i;
+        NSV(me) = e[j].val;
+        CADD(CNT_SNAPSHOTS, 1u);
+      }
     }
   }
+  ND(NF_SLEN, me) = len;
 }
 
 // commit = the majority-th largest match index, if it is from the current term
@@ -315,25 +374,29 @@ DI void node_event(const Dev& D, X& x, bool is_msg, uint32_t tnode, uint32_t slo
     mterm = MS32(MF_TERM, mi); ma = MS32(MF_A, mi); mb = MS32(MF_B, mi); mc = MS32(MF_C, mi);
     type = hdr & 7u; src = (hdr >> 3) & 7u; me = (hdr >> 6) & 7u; inc = (hdr >> 9) & 255u;
     k = (hdr >> 17) & 63u;
-    MS64(M64_KEY, mi) = ~0ull;
+    LK(slot) = ~0ull;
     x.free_mask |= 1ull << slot;
     x.inflight--;
     rescan_min(D, x);
+    PROF(P_DECODE);
   }
   NC d = load_node(D, x, me);
+  PROF(P_LOAD);
   uint32_t mode = SEND_NONE, peers = 0, rtype = 0, ra = 0, rb = 0, kind;
   const uint32_t others = ((1u << D.n) - 1u) & ~(1u << me);
   if (is_msg) {
     kind = type;
     if (!bit(x.alive, me) || !bit(x.conn, me) || !bit(x.conn, src)) {
-      x.cnt[CNT_DROP_DELIVER]++;
+      CADD(CNT_DROP_DELIVER, 1u);
       rec_node(D, x, 0, 16, me, seq, d);
+      PROF(P_DROP);
       return;
     }
     bool is_reply = (type == M_RV_REP || type == M_AE_REP || type == M_IS_REP);
     if (is_reply && inc != f_inc(d.f)) {
-      x.cnt[CNT_DROP_STALE]++;
+      CADD(CNT_DROP_STALE, 1u);
       rec_node(D, x, 0, 17, me, seq, d);
+      PROF(P_DROP);
       return;
     }
     if (mterm > d.term) {  // step down
@@ -341,6 +404,7 @@ DI void node_event(const Dev& D, X& x, bool is_msg, uint32_t tnode, uint32_t slo
       d.term = mterm;
       d.f = f_set(f_set(f_set(d.f, 4, 4, 15u), 16, 8, 0u), 0, 2, R_F);
       if (was == R_L) reset_timer(D, x, me, d);
+      PROF(P_STEPDOWN);
     }
     const uint32_t role = f_role(d.f), term = d.term;
     switch (type) {
@@ -354,6 +418,7 @@ DI void node_event(const Dev& D, X& x, bool is_msg, uint32_t tnode, uint32_t slo
           reset_timer(D, x, me, d);
         }
         mode = SEND_REPLY; rtype = M_RV_REP; ra = granted ? 1u : 0u;
+        PROF(P_RVREQ);
       } break;
       case M_RV_REP:
         if (role == R_C && mterm == term && ma) {
@@ -361,7 +426,7 @@ DI void node_event(const Dev& D, X& x, bool is_msg, uint32_t tnode, uint32_t slo
           d.f = f_set(d.f, 16, 8, votes);
           if ((uint32_t)__builtin_popcount(votes) > D.n / 2) {  // become leader
             d.f = f_set(d.f, 0, 2, R_L);
-            x.cnt[CNT_LEADERS]++;
+            CADD(CNT_LEADERS, 1u);
             for (uint32_t p = 0; p < D.n; p++) {
               PR(PF_NEXT, me, p) = d.last + 1;
               PR(PF_MATCH, me, p) = (p == me) ? d.last : 0u;
@@ -370,6 +435,7 @@ DI void node_event(const Dev& D, X& x, bool is_msg, uint32_t tnode, uint32_t slo
             mode = SEND_APPEND; peers = others;
           }
         }
+        PROF(P_RVREP);
         break;
       case M_AE_REQ: {
         mode = SEND_REPLY; rtype = M_AE_REP;
@@ -390,21 +456,32 @@ DI void node_event(const Dev& D, X& x, bool is_msg, uint32_t tnode, uint32_t slo
           rb = xx;
           break;
         }
-        size_t pb = ((size_t)x.c * D.M + slot) * D.K;
-        for (uint32_t j = j0; j < k; j++) {
-          uint32_t i = ma + 1 + j, et = D.pterm[pb + j];
-          if (i <= d.last && term_at(D, x, me, d, i) == et) continue;
-          if (i - d.snap > D.log_cap) { fail(D, x, MR_FAIL_SIM_CAPACITY); return; }
-          size_t li = logi(D, x, me, i);
-          D.lterm[li] = et;
-          D.lval[li] = D.pval[pb + j];
-          d.last = i;
-          if (i - d.snap > x.cnt[CNT_MAX_LOG]) x.cnt[CNT_MAX_LOG] = i - d.snap;
+        const LE* pp = D.pay + ((size_t)x.c * D.M + slot) * D.K;
+        for (uint32_t j = j0; j < k; j += AC) {  // batches of independent loads
+          LE pe[AC];
+          uint32_t lt[AC];
+#pragma unroll
+          for (uint32_t q = 0; q < AC; q++) {
+            const uint32_t jx = j + q, i = ma + 1 + jx;
+            pe[q] = jx < k ? pp[jx] : LE{};
+            lt[q] = (jx < k && i <= d.last) ? term_at(D, x, me, d, i) : 0u;
+          }
+#pragma unroll
+          for (uint32_t q = 0; q < AC; q++) {
+            const uint32_t jx = j + q, i = ma + 1 + jx;
+            if (jx >= k) break;
+            if (i <= d.last && lt[q] == pe[q].term) continue;  // d.last only drops below i here
+            if (i - d.snap > D.log_cap) { fail(D, x, MR_FAIL_SIM_CAPACITY); return; }
+            D.log[logi(D, x, me, i)] = pe[q];
+            d.last = i;
+            CMAX(CNT_MAX_LOG, i - d.snap);
+          }
         }
         uint32_t lc = ma + k;
         if (mc < lc) lc = mc;
         if (lc > d.commit) d.commit = lc;
         ra = 1; rb = ma + k;
+        PROF(P_AEREQ);
       } break;
       case M_AE_REP:
         if (role != R_L || mterm != term) break;
@@ -418,6 +495,7 @@ DI void node_event(const Dev& D, X& x, bool is_msg, uint32_t tnode, uint32_t slo
           PR(PF_NEXT, me, src) = xx;
           peers = 1u << src;
         }
+        PROF(P_AEREP);
         break;
       case M_IS_REQ: {
         mode = SEND_REPLY; rtype = M_IS_REP;
@@ -431,32 +509,37 @@ DI void node_event(const Dev& D, X& x, bool is_msg, uint32_t tnode, uint32_t slo
           d.commit = idx; d.applied = idx;
           storage_snapshot(D, x, me, idx);
           if (x.code != RUN) return;
-          x.cnt[CNT_INSTALLS]++;
+          CADD(CNT_INSTALLS, 1u);
         }
         rb = idx;
+        PROF(P_ISREQ);
       } break;
       case M_IS_REP:
         if (role == R_L && mterm == term && mb > 0) {
           mode = SEND_APPEND;
           peers = on_ack(D, x, me, d, src, mb);
         }
+        PROF(P_ISREP);
         break;
     }
   } else if (f_role(d.f) == R_L) {  // heartbeat / replication round
     kind = 1;
     set_timer(x, me, x.now + D.hb);
     mode = SEND_APPEND; peers = others;
+    PROF(P_HB);
   } else {  // election timeout: become candidate
     kind = 0;
     d.term++;
     d.f = f_set(f_set(f_set(d.f, 4, 4, me), 0, 2, R_C), 16, 8, 1u << me);
-    x.cnt[CNT_ELECTIONS]++;
+    CADD(CNT_ELECTIONS, 1u);
     reset_timer(D, x, me, d);
     mode = SEND_VOTE; peers = others;
+    PROF(P_ELECT);
   }
   if (d.applied < d.commit) {  // committed entries reach the tester's applier
     node_apply(D, x, me, d);
     if (x.code != RUN) return;
+    PROF(P_APPLY);
   }
   if (mode == SEND_REPLY) peers = 1u << src;
   const uint32_t lt = mode == SEND_VOTE ? term_at(D, x, me, d, d.last) : 0u;
@@ -476,22 +559,28 @@ DI void node_event(const Dev& D, X& x, bool is_msg, uint32_t tnode, uint32_t slo
         sk = d.last - prev;
         if (sk > D.K) sk = D.K;
         st = M_AE_REQ; sa = prev; sb = term_at(D, x, me, d, prev); sc = d.commit;
-        x.cnt[CNT_SHIPPED] += sk;
+        CADD(CNT_SHIPPED, sk);
       }
     }
     int s = net_send(D, x, me, d, p, st, sinc, d.term, sa, sb, sc, sv, sk);
     if (x.code != RUN) return;
-    if (s >= 0 && sk) {
-      size_t pb = ((size_t)x.c * D.M + (uint32_t)s) * D.K;
-      for (uint32_t j = 0; j < sk; j++) {
-        size_t li = logi(D, x, me, prev + 1 + j);
-        D.pterm[pb + j] = D.lterm[li];
-        D.pval[pb + j] = D.lval[li];
+    if (s >= 0 && sk) {  // the payload: entries prev+1 .. prev+sk, batches of AC
+      LE* pp = D.pay + ((size_t)x.c * D.M + (uint32_t)s) * D.K;
+      for (uint32_t j = 0; j < sk; j += AC) {
+        LE t[AC];
+#pragma unroll
+        for (uint32_t q = 0; q < AC; q++)
+          if (j + q < sk) t[q] = D.log[logi(D, x, me, prev + 1 + j + q)];
+#pragma unroll
+        for (uint32_t q = 0; q < AC; q++)
+          if (j + q < sk) pp[j + q] = t[q];
       }
     }
   }
+  PROF(P_SEND);
   store_node(D, x, me, d);
   rec_node(D, x, is_msg ? 0u : 1u, kind, me, is_msg ? seq : 0u, d);
+  PROF(P_STORE);
 }
 
 // ---------------------------------------------------------------- tester API (tester.rs)
@@ -529,10 +618,9 @@ DI bool t_start(const Dev& D, X& x, uint32_t i, uint64_t v, uint32_t& idx, uint3
   if (last - snap > D.log_cap) { fail(D, x, MR_FAIL_SIM_CAPACITY); return false; }
   size_t li = logi(D, x, i, last);
   term = ND(NF_TERM, i);
-  D.lterm[li] = term;
-  D.lval[li] = v;
+  D.log[li] = LE{term, 0u, v};
   ND(NF_LAST, i) = last;
-  if (last - snap > x.cnt[CNT_MAX_LOG]) x.cnt[CNT_MAX_LOG] = last - snap;
+  CMAX(CNT_MAX_LOG, last - snap);
   PR(PF_MATCH, i, i) = last;
   idx = last;
   return true;
@@ -634,9 +722,15 @@ constexpr uint32_t CLS_MSG = 0, CLS_TIMER = 1, CLS_TESTER = 2, CLS_NONE = 3;
 #ifndef MR_WAVES_PER_EU
 #define MR_WAVES_PER_EU 2
 #endif
-__global__ void __launch_bounds__(256, MR_WAVES_PER_EU) step_kernel(Dev D, uint32_t budget) {
+__global__ void __launch_bounds__(STEP_BLOCK, MR_WAVES_PER_EU) step_kernel(Dev D, uint32_t budget) {
   X x;
   x.c = blockIdx.x * blockDim.x + threadIdx.x;
+#ifdef MR_PROF
+  if ((threadIdx.x & 63) == 0) {
+    for (uint32_t k = 0; k < 2 * P__N; k++) s_prof[threadIdx.x >> 6][k] = 0;
+    s_prof[threadIdx.x >> 6][2 * P__N] = wall_clock64();
+  }
+#endif
   const bool in = x.c < D.C;
   x.code = in ? CS(CS_CODE) : (uint32_t)MR_PASS;
   if (x.code == RUN) {
@@ -647,15 +741,20 @@ __global__ void __launch_bounds__(256, MR_WAVES_PER_EU) step_kernel(Dev D, uint3
 #pragma unroll
     for (uint32_t d = 0; d < MR_MAX_NODES; d++) x.timer[d] = d < D.n ? ND(NF_TIMER, d) : INF_T;
     x.free_mask = C64(C64_FREE); x.digest = C64(C64_DIGEST); x.mmin = C64(C64_MMIN);
+#if !MR_CNT_MEM
 #pragma unroll
     for (uint32_t k = 0; k < CNT__N; k++) x.cnt[k] = CS(CS_CNT + k);
+#endif
+    for (uint32_t s = 0; s < D.M; s++) LK(s) = MS64(M64_KEY, s * D.C + x.c);
   }
   const bool live = x.code == RUN;
+  PROF(P_PRO);
   uint64_t key = 0;
   uint32_t cls = CLS_NONE, node = 0;
   bool need = true;
   for (uint32_t it = 0; it < budget; it++) {
     asm volatile("" : "+v"(x.c));  // no LICM of per-lane addresses: recompute, do not keep live
+    PROF(P_TAIL);
     const bool run = x.code == RUN;
     if (__ballot(run) == 0) break;
     if (run && need) {  // next event: min over tester wake-up, node timers, earliest message
@@ -683,19 +782,29 @@ __global__ void __launch_bounds__(256, MR_WAVES_PER_EU) step_kernel(Dev D, uint3
     const bool tpick = MR_TESTER_DEN * ns >= MR_TESTER_NUM * (nm + nt + ns);
     const uint32_t pick = tpick ? CLS_TESTER : (nm >= nt ? CLS_MSG : CLS_TIMER);
     const bool mine = MR_MERGE_NODE ? (tpick ? cls == CLS_TESTER : cls != CLS_TESTER) : cls == pick;
+    PROF(P_SEL);
     if (!run || !mine) continue;
     x.now = (uint32_t)(key >> 32);
     need = true;
     x.events++;
     if (x.events > D.max_events) { fail(D, x, MR_FAIL_SIM_EVENT_LIMIT); continue; }
     if (cls != CLS_TESTER) {
-      x.cnt[cls == CLS_MSG ? CNT_EV_MSG : CNT_EV_TIMER]++;
+      CADD(cls == CLS_MSG ? CNT_EV_MSG : CNT_EV_TIMER, 1u);
       node_event(D, x, cls == CLS_MSG, node, x.mslot, (uint32_t)key & 0x3FFFFFFFu);
     } else {
-      x.cnt[CNT_EV_TESTER]++;
+      CADD(CNT_EV_TESTER, 1u);
       tester(D, x);
+      PROF(P_TESTER);
     }
   }
+#ifdef MR_PROF
+  PROF(P_TAIL);
+  if ((threadIdx.x & 63) == 0)
+    for (uint32_t k = 0; k < P__N; k++) {
+      atomicAdd(&D.prof[k], s_prof[threadIdx.x >> 6][k]);
+      atomicAdd(&D.prof[32 + k], s_prof[threadIdx.x >> 6][P__N + k]);
+    }
+#endif
   if (!live) return;
   CS(CS_CODE) = x.code;
   if (x.code != RUN) CS(CS_VTIME) = x.now;
@@ -707,8 +816,11 @@ __global__ void __launch_bounds__(256, MR_WAVES_PER_EU) step_kernel(Dev D, uint3
   for (uint32_t d = 0; d < MR_MAX_NODES; d++)
     if (d < D.n) ND(NF_TIMER, d) = x.timer[d];
   C64(C64_FREE) = x.free_mask; C64(C64_DIGEST) = x.digest; C64(C64_MMIN) = x.mmin;
+#if !MR_CNT_MEM
 #pragma unroll
   for (uint32_t k = 0; k < CNT__N; k++) CS(CS_CNT + k) = x.cnt[k];
+#endif
+  for (uint32_t s = 0; s < D.M; s++) MS64(M64_KEY, s * D.C + x.c) = LK(s);
   if (x.code == RUN) atomicAdd(D.remaining, 1u);
 }
 
@@ -769,8 +881,9 @@ __global__ void __launch_bounds__(256) reduce_kernel(Dev D, unsigned long long* 
 }
 
 hipError_t launch_step(const Dev& D, uint32_t budget, hipStream_t s) {
-  dim3 blk(256), grd((D.C + 255) / 256);
-  hipLaunchKernelGGL(step_kernel, grd, blk, 0, s, D, budget);
+  dim3 blk(STEP_BLOCK), grd((D.C + STEP_BLOCK - 1) / STEP_BLOCK);
+  hipLaunchKernelGGL(step_kernel, grd, blk, (size_t)D.M * STEP_BLOCK * sizeof(uint64_t), s, D,
+                     budget);
   return hipGetLastError();
 }
 hipError_t launch_reset(const Dev& D, hipStream_t s) {
