@@ -47,7 +47,7 @@ enum : uint32_t { C64_FREE, C64_DIGEST, C64_MMIN, C64_THV, C64_TV, C64__N = C64_
 // nd32 [NF__N][n][C]: per-node u32 fields
 enum : uint32_t {
   NF_FLAGS, NF_TERM, NF_COMMIT, NF_APPLIED, NF_LAST, NF_SNAP, NF_SNAPT, NF_TIMER, NF_ECTR,
-  NF_NCTR, NF_SLEN, NF__N
+  NF_NCTR, NF_SLEN, NF_PEXP, NF_PLO, NF_PHI, NF__N
 };
 // pr32 [PF__N][n][n][C]: leader -> peer
 enum : uint32_t { PF_NEXT, PF_MATCH, PF__N };

@@ -65,7 +65,8 @@ extern __shared__ uint64_t s_keys[];
 // partition each wave's time; slot 32 + k counts the marks.
 enum : uint32_t {
   P_TAIL, P_SEL, P_DECODE, P_LOAD, P_DROP, P_RVREQ, P_RVREP, P_AEREQ, P_AEREP, P_ISREQ, P_ISREP,
-  P_HB, P_ELECT, P_APPLY, P_SEND, P_STORE, P_TESTER, P_STEPDOWN, P_PRO, P_EPI, P__N
+  P_HB, P_ELECT, P_APPLY, P_SEND, P_STORE, P_TESTER, P_STEPDOWN, P_PRO, P_EPI,
+  P_S_SETUP, P_S_NET, P_S_PAY, P_AE_PROBE, P_AP_LOAD, P_AP_CHECK, P__N
 };
 #ifdef MR_PROF
 __shared__ unsigned long long s_prof[STEP_BLOCK / 64][2 * P__N + 1];
@@ -128,6 +129,10 @@ DI void set_timer(X& x, uint32_t d, uint32_t t) {
 __device__ __forceinline__ uint2 philox2(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t k0,
                                       uint32_t k1) {
   uint32_t c3 = 0;
+#ifdef MR_DEV_CHEAP_RNG  // timing experiments only: NOT the simulator's RNG (breaks parity)
+  c0 = (c0 ^ k0) * 0x9E3779B9u ^ (c1 + k1) * 0x85EBCA6Bu ^ c2 * 0xC2B2AE35u;
+  return make_uint2(c0, c0 * 0x27D4EB2Fu + c2);
+#endif
 #pragma unroll
   for (int r = 0; r < 10; r++) {
     uint32_t hi0 = __umulhi(0xD2511F53u, c0), lo0 = 0xD2511F53u * c0;
@@ -153,19 +158,21 @@ DI size_t logi(const Dev& D, const X& x, uint32_t d, uint32_t i) {
 // One node's scalar state, loaded into registers at the start of an event
 // (one batch of independent loads) and stored back at its end.
 struct NC {
-  uint32_t f, term, commit, applied, last, snap, snapt, ectr, nctr;
+  uint32_t f, term, commit, applied, last, snap, snapt, ectr, nctr, pexp;
 };
 DI NC load_node(const Dev& D, const X& x, uint32_t d) {
   NC n;
   n.f = ND(NF_FLAGS, d); n.term = ND(NF_TERM, d); n.commit = ND(NF_COMMIT, d);
   n.applied = ND(NF_APPLIED, d); n.last = ND(NF_LAST, d); n.snap = ND(NF_SNAP, d);
   n.snapt = ND(NF_SNAPT, d); n.ectr = ND(NF_ECTR, d); n.nctr = ND(NF_NCTR, d);
+  n.pexp = ND(NF_PEXP, d);
   return n;
 }
 DI void store_node(const Dev& D, const X& x, uint32_t d, const NC& n) {
   ND(NF_FLAGS, d) = n.f; ND(NF_TERM, d) = n.term; ND(NF_COMMIT, d) = n.commit;
   ND(NF_APPLIED, d) = n.applied; ND(NF_LAST, d) = n.last; ND(NF_SNAP, d) = n.snap;
   ND(NF_SNAPT, d) = n.snapt; ND(NF_ECTR, d) = n.ectr; ND(NF_NCTR, d) = n.nctr;
+  ND(NF_PEXP, d) = n.pexp;
 }
 DI uint32_t term_at(const Dev& D, const X& x, uint32_t d, const NC& n, uint32_t i) {
   if (i == 0) return 0;
@@ -259,6 +266,58 @@ DI int net_send(const Dev& D, X& x, uint32_t src, NC& s, uint32_t dst, uint32_t 
   return (int)slot;
 }
 
+// ---------------------------------------------------------------- zero-copy payloads
+// An AppendEntries message does not copy its entries at send time: the
+// receiver reads them from the sender's log ring at delivery. That is exact as
+// long as the sender does not overwrite a ring slot an in-flight message still
+// references, so each node keeps the index range [PLO, PHI] its unmaterialized
+// messages reference and a deadline PEXP by which all of them are delivered
+// (send time + the 27 ms latency bound). A log write that would overwrite a
+// referenced slot first materializes (copies) those messages' payloads into
+// their slots — rare: it takes a deposed leader whose entries are replaced, or
+// a ring that wraps under in-flight messages.
+constexpr uint32_t HDR_MAT = 1u << 23;  // message header: payload copied into D.pay
+constexpr uint32_t LAT_BOUND_US = 27000u;
+
+DI void pend_note(const Dev& D, X& x, uint32_t me, NC& d, uint32_t lo, uint32_t hi) {
+  uint32_t plo = lo, phi = hi;
+  if (x.now <= d.pexp) {
+    uint32_t olo = ND(NF_PLO, me), ohi = ND(NF_PHI, me);
+    if (olo <= ohi) { plo = olo < lo ? olo : lo; phi = ohi > hi ? ohi : hi; }
+  }
+  ND(NF_PLO, me) = plo;
+  ND(NF_PHI, me) = phi;
+  d.pexp = x.now + LAT_BOUND_US;
+}
+
+// copy the payload of every unmaterialized AppendEntries from node L still in flight
+DI void materialize(const Dev& D, X& x, uint32_t L) {
+  uint64_t occ = ~x.free_mask & (D.M >= 64 ? ~0ull : ((1ull << D.M) - 1ull));
+  while (occ) {
+    const uint32_t s = (uint32_t)__builtin_ctzll(occ);
+    occ &= occ - 1ull;
+    const uint32_t mi = s * D.C + x.c, hdr = MS32(MF_HDR, mi), k = (hdr >> 17) & 63u;
+    if ((hdr & 7u) != M_AE_REQ || ((hdr >> 3) & 7u) != L || (hdr & HDR_MAT) || k == 0) continue;
+    const uint32_t prev = MS32(MF_A, mi);
+    LE* pp = D.pay + ((size_t)x.c * D.M + s) * D.K;
+    for (uint32_t j = 0; j < k; j++) pp[j] = D.log[logi(D, x, L, prev + 1 + j)];
+    MS32(MF_HDR, mi) = hdr | HDR_MAT;
+  }
+  ND(NF_PLO, L) = 1u;  // empty range
+  ND(NF_PHI, L) = 0u;
+}
+
+// before node L (pending deadline pexp) overwrites log index i
+DI void guard_log_write(const Dev& D, X& x, uint32_t L, uint32_t& pexp, uint32_t i) {
+  if (x.now > pexp) return;  // every message L sent has been delivered
+  const uint32_t plo = ND(NF_PLO, L), phi = ND(NF_PHI, L);
+  if (plo > phi) return;
+  const uint32_t span = phi - plo;  // referenced j in [plo, phi] shares i's slot iff j = i mod cap
+  if (span < D.log_cap - 1u && ((i - plo) & (D.log_cap - 1u)) > span) return;
+  materialize(D, x, L);
+  pexp = 0;
+}
+
 // ---------------------------------------------------------------- tester storage
 constexpr uint32_t AC = 4;  // entries per batch of independent loads in log walks
 DI void storage_snapshot(const Dev& D, X& x, uint32_t i, uint32_t idx) {  // tester.rs:399-402
@@ -311,6 +370,7 @@ DI void node_apply(const Dev& D, X& x, uint32_t me, NC& d) {
       m[j] = ok ? D.smask[sb + i] : 0u;
       sv[j] = ok ? D.sval[sb + i] : 0ull;
     }
+    PROF(P_AP_LOAD);
 #pragma unroll
     for (uint32_t j = 0; j < AC; j++) {
       const uint32_t i = i0 + j;
@@ -333,6 +393,7 @@ DI void node_apply(const Dev& D, X& x, uint32_t me, NC& d) {
         CADD(CNT_SNAPSHOTS, 1u);
       }
     }
+    PROF(P_AP_CHECK);
   }
   ND(NF_SLEN, me) = len;
 }
@@ -367,13 +428,14 @@ DI uint32_t on_ack(const Dev& D, X& x, uint32_t me, NC& d, uint32_t p, uint32_t 
 DI void node_event(const Dev& D, X& x, bool is_msg, uint32_t tnode, uint32_t slot,
                    uint32_t seq) {
   uint32_t me = tnode, src = 0, type = 0, inc = 0, k = 0, mterm = 0, ma = 0, mb = 0, mc = 0;
-  uint32_t mi = 0;
+  uint32_t mi = 0, hdr_bits = 0;
   if (is_msg) {
     mi = slot * D.C + x.c;
     uint32_t hdr = MS32(MF_HDR, mi);
     mterm = MS32(MF_TERM, mi); ma = MS32(MF_A, mi); mb = MS32(MF_B, mi); mc = MS32(MF_C, mi);
     type = hdr & 7u; src = (hdr >> 3) & 7u; me = (hdr >> 6) & 7u; inc = (hdr >> 9) & 255u;
     k = (hdr >> 17) & 63u;
+    hdr_bits = hdr;
     LK(slot) = ~0ull;
     x.free_mask |= 1ull << slot;
     x.inflight--;
@@ -450,6 +512,7 @@ DI void node_event(const Dev& D, X& x, bool is_msg, uint32_t tnode, uint32_t slo
         }
         if (prev > d.last) { rb = d.last + 1; break; }
         uint32_t tp = term_at(D, x, me, d, prev);
+        PROF(P_AE_PROBE);
         if (tp != pterm) {
           uint32_t xx = prev;
           while (xx - 1 > d.snap && term_at(D, x, me, d, xx - 1) == tp) xx--;
@@ -457,13 +520,14 @@ DI void node_event(const Dev& D, X& x, bool is_msg, uint32_t tnode, uint32_t slo
           break;
         }
         const LE* pp = D.pay + ((size_t)x.c * D.M + slot) * D.K;
+        const bool mat = (hdr_bits & HDR_MAT) != 0u;
         for (uint32_t j = j0; j < k; j += AC) {  // batches of independent loads
           LE pe[AC];
           uint32_t lt[AC];
 #pragma unroll
           for (uint32_t q = 0; q < AC; q++) {
             const uint32_t jx = j + q, i = ma + 1 + jx;
-            pe[q] = jx < k ? pp[jx] : LE{};
+            pe[q] = jx < k ? (mat ? pp[jx] : D.log[logi(D, x, src, i)]) : LE{};
             lt[q] = (jx < k && i <= d.last) ? term_at(D, x, me, d, i) : 0u;
           }
 #pragma unroll
@@ -472,6 +536,7 @@ DI void node_event(const Dev& D, X& x, bool is_msg, uint32_t tnode, uint32_t slo
             if (jx >= k) break;
             if (i <= d.last && lt[q] == pe[q].term) continue;  // d.last only drops below i here
             if (i - d.snap > D.log_cap) { fail(D, x, MR_FAIL_SIM_CAPACITY); return; }
+            guard_log_write(D, x, me, d.pexp, i);
             D.log[logi(D, x, me, i)] = pe[q];
             d.last = i;
             CMAX(CNT_MAX_LOG, i - d.snap);
@@ -543,6 +608,7 @@ DI void node_event(const Dev& D, X& x, bool is_msg, uint32_t tnode, uint32_t slo
   }
   if (mode == SEND_REPLY) peers = 1u << src;
   const uint32_t lt = mode == SEND_VOTE ? term_at(D, x, me, d, d.last) : 0u;
+  uint32_t plo_acc = ~0u, phi_acc = 0u;  // index range referenced by this event's payloads
   while (peers) {  // the single send path: ascending peer order
     uint32_t p = (uint32_t)__builtin_ctz(peers);
     peers &= peers - 1u;
@@ -562,21 +628,17 @@ DI void node_event(const Dev& D, X& x, bool is_msg, uint32_t tnode, uint32_t slo
         CADD(CNT_SHIPPED, sk);
       }
     }
+    PROF(P_S_SETUP);
     int s = net_send(D, x, me, d, p, st, sinc, d.term, sa, sb, sc, sv, sk);
     if (x.code != RUN) return;
-    if (s >= 0 && sk) {  // the payload: entries prev+1 .. prev+sk, batches of AC
-      LE* pp = D.pay + ((size_t)x.c * D.M + (uint32_t)s) * D.K;
-      for (uint32_t j = 0; j < sk; j += AC) {
-        LE t[AC];
-#pragma unroll
-        for (uint32_t q = 0; q < AC; q++)
-          if (j + q < sk) t[q] = D.log[logi(D, x, me, prev + 1 + j + q)];
-#pragma unroll
-        for (uint32_t q = 0; q < AC; q++)
-          if (j + q < sk) pp[j + q] = t[q];
-      }
+    PROF(P_S_NET);
+    if (s >= 0 && sk) {  // zero-copy payload: entries prev+1 .. prev+sk stay in this log
+      plo_acc = prev + 1 < plo_acc ? prev + 1 : plo_acc;
+      phi_acc = prev + sk > phi_acc ? prev + sk : phi_acc;
+      PROF(P_S_PAY);
     }
   }
+  if (plo_acc <= phi_acc) pend_note(D, x, me, d, plo_acc, phi_acc);
   PROF(P_SEND);
   store_node(D, x, me, d);
   rec_node(D, x, is_msg ? 0u : 1u, kind, me, is_msg ? seq : 0u, d);
@@ -618,6 +680,9 @@ DI bool t_start(const Dev& D, X& x, uint32_t i, uint64_t v, uint32_t& idx, uint3
   if (last - snap > D.log_cap) { fail(D, x, MR_FAIL_SIM_CAPACITY); return false; }
   size_t li = logi(D, x, i, last);
   term = ND(NF_TERM, i);
+  uint32_t pexp = ND(NF_PEXP, i);
+  guard_log_write(D, x, i, pexp, last);
+  ND(NF_PEXP, i) = pexp;
   D.log[li] = LE{term, 0u, v};
   ND(NF_LAST, i) = last;
   CMAX(CNT_MAX_LOG, last - snap);
@@ -840,6 +905,7 @@ __global__ void __launch_bounds__(256) reset_kernel(Dev D) {
     ND(NF_FLAGS, d) = 15u << 4;  // follower, voted none (down, disconnected: CS_ALIVE/CS_CONN = 0)
     ND(NF_TIMER, d) = INF_T;
     ND(NF_SLEN, d) = 1;
+    ND(NF_PLO, d) = 1;  // no pending payload range
     NSV(d) = 0;
     for (uint32_t p = 0; p < D.n; p++) { PR(PF_NEXT, d, p) = 0; PR(PF_MATCH, d, p) = 0; }
   }
