@@ -22,22 +22,55 @@ def _stale(out, srcs):
     return any(os.path.getmtime(s) > t for s in srcs)
 
 
-def build_hip(force=False, verbose=False):
-    srcs = sorted(glob.glob(os.path.join(HERE, "csrc", "*.hip")) +
-                  glob.glob(os.path.join(HERE, "csrc", "*.cpp")))
-    deps = srcs + glob.glob(os.path.join(HERE, "csrc", "*.h")) + \
-        glob.glob(os.path.join(HERE, "csrc", "*.inc")) + \
-        [os.path.join(ROOT, "include", "madraft_sim.h")]
-    if not force and not _stale(LIB, deps):
-        return LIB
-    os.makedirs(os.path.dirname(LIB), exist_ok=True)
-    cmd = ["hipcc", f"--offload-arch={ARCH}", "-O3", "-fPIC", "-shared", "-std=c++17",
-           "-Wall", "-Wno-unused-function", *srcs, "-o", LIB + ".tmp"]
+# step-kernel instances (one per scenario id, mr_dev.h MR_ALL_SCNS) are split
+# over several translation units of mr_kernel.hip compiled in parallel
+SCN_IDS = [1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 16, 19, 20, 21, 22, 23, 24]
+N_GROUPS = 7
+
+
+def _units(csrc):
+    kern = os.path.join(csrc, "mr_kernel.hip")
+    units = [(kern, "common", ["-DMR_COMMON=1", "-DMR_SCN_LIST="])]
+    for g in range(N_GROUPS):
+        ids = SCN_IDS[g::N_GROUPS]
+        lst = " ".join(f"MR_INST({i})" for i in ids)
+        units.append((kern, f"scn{g}", ["-DMR_COMMON=0", f"-DMR_SCN_LIST={lst}"]))
+    for src in sorted(glob.glob(os.path.join(csrc, "*.cpp"))):
+        units.append((src, os.path.splitext(os.path.basename(src))[0], []))
+    return units
+
+
+def build_hip(force=False, verbose=False, extra=(), out=None):
+    """Compile the product library; `extra` flags / `out` path for dev variants."""
+    out = out or LIB
+    csrc = os.path.join(HERE, "csrc")
+    srcs = sorted(glob.glob(os.path.join(csrc, "*.hip")) + glob.glob(os.path.join(csrc, "*.cpp")))
+    deps = srcs + glob.glob(os.path.join(csrc, "*.h")) + glob.glob(os.path.join(csrc, "*.inc")) + \
+        [os.path.join(ROOT, "include", "madraft_sim.h"), os.path.abspath(__file__)]
+    if not force and not extra and not _stale(out, deps):
+        return out
+    objdir = os.path.join(HERE, "lib", "obj" + ("_" + os.path.basename(out) if out != LIB else ""))
+    os.makedirs(objdir, exist_ok=True)
+    base = ["hipcc", f"--offload-arch={ARCH}", "-O3", "-fPIC", "-std=c++17", "-Wall",
+            "-Wno-unused-function", *extra]
+    jobs, objs = [], []
+    for src, name, flags in _units(csrc):
+        obj = os.path.join(objdir, name + ".o")
+        objs.append(obj)
+        cmd = base + flags + ["-c", src, "-o", obj]
+        if verbose:
+            print(" ".join(cmd))
+        jobs.append((cmd, subprocess.Popen(cmd)))
+    bad = [c for c, p in jobs if p.wait() != 0]
+    if bad:
+        raise RuntimeError("hipcc failed: " + " ".join(bad[0]))
+    os.makedirs(os.path.dirname(out), exist_ok=True)
+    cmd = ["hipcc", f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, "-o", out + ".tmp"]
     if verbose:
         print(" ".join(cmd))
     subprocess.run(cmd, check=True)
-    os.replace(LIB + ".tmp", LIB)
-    return LIB
+    os.replace(out + ".tmp", out)
+    return out
 
 
 def build_oracle(verbose=False):

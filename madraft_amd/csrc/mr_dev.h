@@ -11,6 +11,7 @@
 // rings, message payloads, the tester's apply checker — is cluster-major so
 // each lane's walk stays in its own cache lines (64-bit offsets).
 #pragma once
+#include <hip/hip_runtime.h>
 #include <stdint.h>
 
 #include "../../include/madraft_sim.h"
@@ -84,5 +85,13 @@ struct Dev {
   unsigned long long* prof;  // [PROF_SLOTS] wave-cycle profile (MR_PROF builds only)
 };
 constexpr uint32_t PROF_SLOTS = 64;
+
+// one step-kernel instance per scenario (mr_kernel.hip launch_step_t<S>)
+template <uint32_t S>
+hipError_t launch_step_t(const Dev& D, uint32_t budget, hipStream_t s);
+#define MR_ALL_SCNS                                                                       \
+  MR_INST(1) MR_INST(2) MR_INST(3) MR_INST(4) MR_INST(5) MR_INST(6) MR_INST(7) MR_INST(8) \
+  MR_INST(9) MR_INST(10) MR_INST(11) MR_INST(12) MR_INST(13) MR_INST(14) MR_INST(16)      \
+  MR_INST(19) MR_INST(20) MR_INST(21) MR_INST(22) MR_INST(23) MR_INST(24)
 
 }  // namespace mr

@@ -15,7 +15,16 @@
 #include "mr_dev.h"
 
 namespace mr {
-hipError_t launch_step(const Dev& D, uint32_t budget, hipStream_t s);
+// the step-kernel instance of scenario `scn` (instances: MR_ALL_SCNS)
+hipError_t launch_step(const Dev& D, uint32_t scn, uint32_t budget, hipStream_t s) {
+  switch (scn) {
+#define MR_INST(S) \
+  case S: return launch_step_t<S>(D, budget, s);
+    MR_ALL_SCNS
+#undef MR_INST
+    default: return hipErrorInvalidValue;
+  }
+}
 hipError_t launch_reset(const Dev& D, hipStream_t s);
 hipError_t launch_reduce(const Dev& D, unsigned long long* out, uint64_t cluster_base,
                          hipStream_t s);
@@ -276,7 +285,7 @@ int mr_batch_run(mr_batch* b, uint64_t max_events_per_call, mr_run_stats* st) {
     }
     HIPCHK(hipMemsetAsync(b->D.remaining, 0, sizeof(uint32_t), b->stream));
     HIPCHK(hipEventRecord(b->ev0, b->stream));
-    HIPCHK(launch_step(b->D, budget, b->stream));
+    HIPCHK(launch_step(b->D, b->D.scenario, budget, b->stream));
     HIPCHK(hipEventRecord(b->ev1, b->stream));
     HIPCHK(hipMemcpyAsync(b->h_remaining, b->D.remaining, sizeof(uint32_t), hipMemcpyDeviceToHost,
                           b->stream));

@@ -28,7 +28,8 @@ namespace mr {
 #define DI __device__ __forceinline__
 constexpr uint32_t INF_T = 0xFFFFFFFFu;
 constexpr uint32_t LOSS_Q32 = 429496729u;  // floor(0.1 * 2^32), tester.rs:130
-constexpr uint64_t FNV_OFF = 0xCBF29CE484222325ull, FNV_P = 0x100000001B3ull;
+[[maybe_unused]] constexpr uint64_t FNV_OFF = 0xCBF29CE484222325ull;
+constexpr uint64_t FNV_P = 0x100000001B3ull;
 constexpr uint32_t RUN = MR_RUNNING;
 constexpr uint32_t NONE = 0xFFFFFFFFu;
 constexpr uint32_t ELECTION_US = 1000000;  // RAFT_ELECTION_TIMEOUT, tests.rs:18
@@ -741,6 +742,7 @@ DI uint32_t nd_term(const Dev& D, X& x, uint32_t i) { return ND(NF_TERM, i); }
 #include "mr_tester.inc"
 
 // one tester event: resume the cluster's coroutine until it sleeps or ends
+template <uint32_t S>
 DI void tester(const Dev& D, X& x) {
   T t;
   uint32_t pcw = CS(CS_TPC);
@@ -763,7 +765,7 @@ DI void tester(const Dev& D, X& x) {
       if (!done) break;  // it slept
       t.helper = H_NONE;
     }
-    run_scenario(D, x, t);
+    run_scenario<S>(D, x, t);
     if (x.code != RUN) return;
     if (x.yield) break;
     if (t.helper == H_NONE) { fail(D, x, MR_FAIL_SIM_BAD_PROGRAM); return; }
@@ -787,6 +789,7 @@ constexpr uint32_t CLS_MSG = 0, CLS_TIMER = 1, CLS_TESTER = 2, CLS_NONE = 3;
 #ifndef MR_WAVES_PER_EU
 #define MR_WAVES_PER_EU 2
 #endif
+template <uint32_t S>
 __global__ void __launch_bounds__(STEP_BLOCK, MR_WAVES_PER_EU) step_kernel(Dev D, uint32_t budget) {
   X x;
   x.c = blockIdx.x * blockDim.x + threadIdx.x;
@@ -858,7 +861,7 @@ __global__ void __launch_bounds__(STEP_BLOCK, MR_WAVES_PER_EU) step_kernel(Dev D
       node_event(D, x, cls == CLS_MSG, node, x.mslot, (uint32_t)key & 0x3FFFFFFFu);
     } else {
       CADD(CNT_EV_TESTER, 1u);
-      tester(D, x);
+      tester<S>(D, x);
       PROF(P_TESTER);
     }
   }
@@ -889,6 +892,10 @@ __global__ void __launch_bounds__(STEP_BLOCK, MR_WAVES_PER_EU) step_kernel(Dev D
   if (x.code == RUN) atomicAdd(D.remaining, 1u);
 }
 
+#ifndef MR_COMMON
+#define MR_COMMON 1
+#endif
+#if MR_COMMON
 // RaftTester state before the test body runs (SEMANTICS §3: tester wakes at t = 0)
 __global__ void __launch_bounds__(256) reset_kernel(Dev D) {
   X x;
@@ -946,12 +953,6 @@ __global__ void __launch_bounds__(256) reduce_kernel(Dev D, unsigned long long* 
   }
 }
 
-hipError_t launch_step(const Dev& D, uint32_t budget, hipStream_t s) {
-  dim3 blk(STEP_BLOCK), grd((D.C + STEP_BLOCK - 1) / STEP_BLOCK);
-  hipLaunchKernelGGL(step_kernel, grd, blk, (size_t)D.M * STEP_BLOCK * sizeof(uint64_t), s, D,
-                     budget);
-  return hipGetLastError();
-}
 hipError_t launch_reset(const Dev& D, hipStream_t s) {
   dim3 blk(256), grd((D.C + 255) / 256);
   hipLaunchKernelGGL(reset_kernel, grd, blk, 0, s, D);
@@ -963,5 +964,23 @@ hipError_t launch_reduce(const Dev& D, unsigned long long* out, uint64_t cluster
   hipLaunchKernelGGL(reduce_kernel, grd, blk, 0, s, D, out, cluster_base);
   return hipGetLastError();
 }
+#endif  // MR_COMMON
+
+template <uint32_t S>
+hipError_t launch_step_t(const Dev& D, uint32_t budget, hipStream_t s) {
+  dim3 blk(STEP_BLOCK), grd((D.C + STEP_BLOCK - 1) / STEP_BLOCK);
+  hipLaunchKernelGGL(step_kernel<S>, grd, blk, (size_t)D.M * STEP_BLOCK * sizeof(uint64_t), s, D,
+                     budget);
+  return hipGetLastError();
+}
+// Step-kernel instances built by this translation unit: build.py compiles
+// this file once per scenario group (-DMR_SCN_LIST=...) in parallel, and once
+// with MR_COMMON=1 for the reset / reduce kernels.
+#ifndef MR_SCN_LIST
+#define MR_SCN_LIST MR_ALL_SCNS
+#endif
+#define MR_INST(S) template hipError_t launch_step_t<S>(const Dev&, uint32_t, hipStream_t);
+MR_SCN_LIST
+#undef MR_INST
 
 }  // namespace mr
