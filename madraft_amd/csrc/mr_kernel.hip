@@ -37,7 +37,7 @@ constexpr uint32_t ELECTION_US = 1000000;  // RAFT_ELECTION_TIMEOUT, tests.rs:18
 // per-lane registers of one cluster during a launch
 struct X {
   uint32_t c, now, events, msgs_sent, inflight, code, trace_n, mslot, netmode, t_ctr;
-  uint32_t sleep_us, yield;
+  uint32_t sleep_us, yield, twake;  // twake: the tester's next wake-up (CS_TWAKE)
   uint32_t conn, alive;  // node bit masks: connected (net clog state), started (tester.rs:24-25)
   uint64_t free_mask, digest, mmin;
   uint32_t timer[MR_MAX_NODES];  // node timers (election / heartbeat deadline), INF_T = none
@@ -60,6 +60,10 @@ struct X {
 constexpr uint32_t STEP_BLOCK = 128;
 extern __shared__ uint64_t s_keys[];
 #define LK(s) s_keys[(s) * STEP_BLOCK + threadIdx.x]
+// send-loop staging after the M keys: next[p] and term at next[p] - 1 (u32)
+#define LNX(p) reinterpret_cast<uint32_t*>(s_keys + D.M * STEP_BLOCK)[(p) * STEP_BLOCK + threadIdx.x]
+#define LPT(p) \
+  reinterpret_cast<uint32_t*>(s_keys + D.M * STEP_BLOCK)[(MR_MAX_NODES + (p)) * STEP_BLOCK + threadIdx.x]
 
 // Development profile (MR_PROF builds): the first active lane of a wave adds
 // the wave cycles since the previous mark to section k, so the sections
@@ -251,11 +255,13 @@ DI int net_send(const Dev& D, X& x, uint32_t src, NC& s, uint32_t dst, uint32_t 
   philox(D, x, ctr, src, ST_NET, w0, w1);
   if (w0 < net_loss(x)) { CADD(CNT_DROP_LOSS, 1u); return -1; }
   if (x.inflight >= D.M) { CADD(CNT_DROP_OVERFLOW, 1u); return -1; }
-  if (seq >= (1u << 30)) { fail(D, x, MR_FAIL_SIM_CAPACITY); return -1; }
+  if (seq >= (1u << 27)) { fail(D, x, MR_FAIL_SIM_CAPACITY); return -1; }  // SEMANTICS §3
   uint32_t t = x.now + u_range(w1, 1000u, net_lat_hi(x));
   uint32_t slot = (uint32_t)__builtin_ctzll(x.free_mask);
   x.free_mask &= ~(1ull << slot);
-  uint64_t key = ((uint64_t)t << 32) | seq;
+  // key = (time, seq, dst): ordered as (time, seq) since seq is unique; dst in
+  // the low bits lets a delivery load the node's state before the message body
+  uint64_t key = ((uint64_t)t << 32) | (seq << 3) | dst;
   uint32_t mi = slot * D.C + x.c;
   LK(slot) = key;
   MS32(MF_HDR, mi) = type | (src << 3) | (dst << 6) | (inc << 9) | (k << 17);
@@ -321,6 +327,10 @@ DI void guard_log_write(const Dev& D, X& x, uint32_t L, uint32_t& pexp, uint32_t
 
 // ---------------------------------------------------------------- tester storage
 constexpr uint32_t AC = 4;  // entries per batch of independent loads in log walks
+#ifndef MR_AC_APPLY
+#define MR_AC_APPLY 8
+#endif
+constexpr uint32_t AC_APPLY = MR_AC_APPLY;  // entries per batch in the applier
 DI void storage_snapshot(const Dev& D, X& x, uint32_t i, uint32_t idx) {  // tester.rs:399-402
   if (idx >= D.apply_cap) { fail(D, x, MR_FAIL_SIM_CAPACITY); return; }
   uint32_t nl = idx + 1, len = ND(NF_SLEN, i);
@@ -360,11 +370,11 @@ DI void node_apply(const Dev& D, X& x, uint32_t me, NC& d) {
   uint32_t len = ND(NF_SLEN, me);
   while (d.applied < d.commit) {
     const uint32_t i0 = d.applied + 1;
-    LE e[AC];
-    uint32_t m[AC];
-    uint64_t sv[AC];
+    LE e[AC_APPLY];
+    uint32_t m[AC_APPLY];
+    uint64_t sv[AC_APPLY];
 #pragma unroll
-    for (uint32_t j = 0; j < AC; j++) {
+    for (uint32_t j = 0; j < AC_APPLY; j++) {
       const uint32_t i = i0 + j;
       const bool ok = i <= d.commit && i < D.apply_cap;
       e[j] = ok ? D.log[logi(D, x, me, i)] : LE{};
@@ -373,7 +383,7 @@ DI void node_apply(const Dev& D, X& x, uint32_t me, NC& d) {
     }
     PROF(P_AP_LOAD);
 #pragma unroll
-    for (uint32_t j = 0; j < AC; j++) {
+    for (uint32_t j = 0; j < AC_APPLY; j++) {
       const uint32_t i = i0 + j;
       if (i > d.commit) break;
       d.applied = i;
@@ -399,12 +409,9 @@ DI void node_apply(const Dev& D, X& x, uint32_t me, NC& d) {
   ND(NF_SLEN, me) = len;
 }
 
-// commit = the majority-th largest match index, if it is from the current term
-DI void advance_commit(const Dev& D, X& x, uint32_t me, NC& d) {
-  uint32_t mv[MR_MAX_NODES];
-#pragma unroll
-  for (uint32_t p = 0; p < MR_MAX_NODES; p++)
-    mv[p] = (p < D.n) ? ((p == me) ? d.last : PR(PF_MATCH, me, p)) : 0u;
+// commit = the majority-th largest of the match indices mv[] (mv[me] = last),
+// if that entry is from the current term
+DI void advance_commit(const Dev& D, X& x, uint32_t me, NC& d, const uint32_t (&mv)[MR_MAX_NODES]) {
   uint32_t maj = D.n / 2 + 1, N = 0;
 #pragma unroll
   for (uint32_t i = 0; i < MR_MAX_NODES; i++) {
@@ -417,13 +424,36 @@ DI void advance_commit(const Dev& D, X& x, uint32_t me, NC& d) {
 }
 
 // AppendEntries / InstallSnapshot acknowledgement up to xv; returns the peer
-// mask to send a follow-up append to
+// mask to send a follow-up append to. The match indices of every peer and
+// next[p] are loaded as one batch of independent loads.
 DI uint32_t on_ack(const Dev& D, X& x, uint32_t me, NC& d, uint32_t p, uint32_t xv) {
-  uint32_t m = PR(PF_MATCH, me, p), nx = PR(PF_NEXT, me, p);
-  if (xv > m) PR(PF_MATCH, me, p) = xv;
+  // constant indices only: a select chain over a per-lane index is turned
+  // back into a dynamically indexed scratch array by the compiler
+  uint32_t mv[MR_MAX_NODES], mp = 0;
+#pragma unroll
+  for (uint32_t q = 0; q < MR_MAX_NODES; q++) {
+    const uint32_t v = (q < D.n && q != me) ? PR(PF_MATCH, me, q) : 0u;
+    mp = (q == p) ? v : mp;
+    mv[q] = (q == me) ? d.last : ((q == p && xv > v) ? xv : v);
+  }
+  uint32_t nx = PR(PF_NEXT, me, p);
+  if (xv > mp) PR(PF_MATCH, me, p) = xv;
   if (xv + 1 > nx) { nx = xv + 1; PR(PF_NEXT, me, p) = nx; }
-  advance_commit(D, x, me, d);
+  advance_commit(D, x, me, d, mv);
   return nx <= d.last ? (1u << p) : 0u;  // still behind: pipeline the next batch
+}
+
+// AC entries j.. of an AppendEntries payload (the sender's ring, or the
+// materialized copy) and the receiver's terms at their indices
+DI void ae_load_batch(const Dev& D, const X& x, uint32_t me, const NC& d, uint32_t src, bool mat,
+                      const LE* pp, uint32_t ma, uint32_t k, uint32_t j, LE (&pe)[AC],
+                      uint32_t (&lt)[AC]) {
+#pragma unroll
+  for (uint32_t q = 0; q < AC; q++) {
+    const uint32_t jx = j + q, i = ma + 1 + jx;
+    pe[q] = jx < k ? (mat ? pp[jx] : D.log[logi(D, x, src, i)]) : LE{};
+    lt[q] = (jx < k && i <= d.last) ? term_at(D, x, me, d, i) : 0u;
+  }
 }
 
 DI void node_event(const Dev& D, X& x, bool is_msg, uint32_t tnode, uint32_t slot,
@@ -434,7 +464,7 @@ DI void node_event(const Dev& D, X& x, bool is_msg, uint32_t tnode, uint32_t slo
     mi = slot * D.C + x.c;
     uint32_t hdr = MS32(MF_HDR, mi);
     mterm = MS32(MF_TERM, mi); ma = MS32(MF_A, mi); mb = MS32(MF_B, mi); mc = MS32(MF_C, mi);
-    type = hdr & 7u; src = (hdr >> 3) & 7u; me = (hdr >> 6) & 7u; inc = (hdr >> 9) & 255u;
+    type = hdr & 7u; src = (hdr >> 3) & 7u; inc = (hdr >> 9) & 255u;  // dst = tnode (key)
     k = (hdr >> 17) & 63u;
     hdr_bits = hdr;
     LK(slot) = ~0ull;
@@ -512,7 +542,14 @@ DI void node_event(const Dev& D, X& x, bool is_msg, uint32_t tnode, uint32_t slo
           prev = d.snap; pterm = d.snapt;
         }
         if (prev > d.last) { rb = d.last + 1; break; }
-        uint32_t tp = term_at(D, x, me, d, prev);
+        const LE* pp = D.pay + ((size_t)x.c * D.M + slot) * D.K;
+        const bool mat = (hdr_bits & HDR_MAT) != 0u;
+        // one batch of independent loads: prev's term, then AC payload entries
+        // (sender's ring or materialized copy) and our terms at their indices
+        LE pe[AC];
+        uint32_t lt[AC];
+        const uint32_t tp = term_at(D, x, me, d, prev);
+        ae_load_batch(D, x, me, d, src, mat, pp, ma, k, j0, pe, lt);
         PROF(P_AE_PROBE);
         if (tp != pterm) {
           uint32_t xx = prev;
@@ -520,17 +557,8 @@ DI void node_event(const Dev& D, X& x, bool is_msg, uint32_t tnode, uint32_t slo
           rb = xx;
           break;
         }
-        const LE* pp = D.pay + ((size_t)x.c * D.M + slot) * D.K;
-        const bool mat = (hdr_bits & HDR_MAT) != 0u;
-        for (uint32_t j = j0; j < k; j += AC) {  // batches of independent loads
-          LE pe[AC];
-          uint32_t lt[AC];
-#pragma unroll
-          for (uint32_t q = 0; q < AC; q++) {
-            const uint32_t jx = j + q, i = ma + 1 + jx;
-            pe[q] = jx < k ? (mat ? pp[jx] : D.log[logi(D, x, src, i)]) : LE{};
-            lt[q] = (jx < k && i <= d.last) ? term_at(D, x, me, d, i) : 0u;
-          }
+        for (uint32_t j = j0; j < k; j += AC) {
+          if (j != j0) ae_load_batch(D, x, me, d, src, mat, pp, ma, k, j, pe, lt);
 #pragma unroll
           for (uint32_t q = 0; q < AC; q++) {
             const uint32_t jx = j + q, i = ma + 1 + jx;
@@ -609,6 +637,27 @@ DI void node_event(const Dev& D, X& x, bool is_msg, uint32_t tnode, uint32_t slo
   }
   if (mode == SEND_REPLY) peers = 1u << src;
   const uint32_t lt = mode == SEND_VOTE ? term_at(D, x, me, d, d.last) : 0u;
+  // appends: next[p] of every peer, then the terms at next[p] - 1, as two
+  // batches of independent loads, staged in LDS for the send loop
+  uint64_t snapv = 0;
+  if (mode == SEND_APPEND) {
+    uint32_t nxa[MR_MAX_NODES];
+    bool any_is = false;
+#pragma unroll
+    for (uint32_t p = 0; p < MR_MAX_NODES; p++) {
+      nxa[p] = bit(peers, p) ? PR(PF_NEXT, me, p) : 0u;
+      any_is |= bit(peers, p) && nxa[p] <= d.snap;
+    }
+#pragma unroll
+    for (uint32_t p = 0; p < MR_MAX_NODES; p++) {
+      const uint32_t pv = nxa[p] - 1u;
+      const bool ld = bit(peers, p) && nxa[p] > d.snap && pv != 0u && pv != d.snap;
+      const uint32_t t = ld ? D.log[logi(D, x, me, pv)].term : 0u;
+      LNX(p) = nxa[p];
+      LPT(p) = (pv == d.snap) ? d.snapt : t;  // term_at(pv); pv == 0 -> 0
+    }
+    if (any_is) snapv = NSV(me);
+  }
   uint32_t plo_acc = ~0u, phi_acc = 0u;  // index range referenced by this event's payloads
   while (peers) {  // the single send path: ascending peer order
     uint32_t p = (uint32_t)__builtin_ctz(peers);
@@ -618,14 +667,14 @@ DI void node_event(const Dev& D, X& x, bool is_msg, uint32_t tnode, uint32_t slo
     if (mode == SEND_REPLY) {
       st = rtype; sa = ra; sb = rb; sc = 0; sinc = inc;
     } else if (mode == SEND_APPEND) {
-      uint32_t nx = PR(PF_NEXT, me, p);
+      const uint32_t nx = LNX(p);
       if (nx <= d.snap) {
-        st = M_IS_REQ; sa = d.snap; sb = d.snapt; sc = 0; sv = NSV(me);
+        st = M_IS_REQ; sa = d.snap; sb = d.snapt; sc = 0; sv = snapv;
       } else {
         prev = nx - 1;
         sk = d.last - prev;
         if (sk > D.K) sk = D.K;
-        st = M_AE_REQ; sa = prev; sb = term_at(D, x, me, d, prev); sc = d.commit;
+        st = M_AE_REQ; sa = prev; sb = LPT(p); sc = d.commit;
         CADD(CNT_SHIPPED, sk);
       }
     }
@@ -773,7 +822,7 @@ DI void tester(const Dev& D, X& x) {
   rec_simple(D, x, 2, 0);  // time::sleep closes this tester segment (SEMANTICS §7)
   uint64_t target = (uint64_t)x.now + x.sleep_us;
   if (target >= INF_T) { fail(D, x, MR_FAIL_SIM_CAPACITY); return; }
-  CS(CS_TWAKE) = (uint32_t)target;
+  x.twake = (uint32_t)target;
   CS(CS_TPC) = t.pc | (t.helper << 24);
   CS(CS_TRES) = t.res;
 #pragma unroll
@@ -805,7 +854,7 @@ __global__ void __launch_bounds__(STEP_BLOCK, MR_WAVES_PER_EU) step_kernel(Dev D
     x.now = CS(CS_NOW); x.events = CS(CS_EVENTS); x.msgs_sent = CS(CS_MSGS);
     x.inflight = CS(CS_INFLIGHT); x.trace_n = CS(CS_TRACEN); x.mslot = CS(CS_MSLOT);
     x.netmode = CS(CS_NETMODE); x.t_ctr = CS(CS_TCTR);
-    x.conn = CS(CS_CONN); x.alive = CS(CS_ALIVE);
+    x.conn = CS(CS_CONN); x.alive = CS(CS_ALIVE); x.twake = CS(CS_TWAKE);
 #pragma unroll
     for (uint32_t d = 0; d < MR_MAX_NODES; d++) x.timer[d] = d < D.n ? ND(NF_TIMER, d) : INF_T;
     x.free_mask = C64(C64_FREE); x.digest = C64(C64_DIGEST); x.mmin = C64(C64_MMIN);
@@ -826,14 +875,14 @@ __global__ void __launch_bounds__(STEP_BLOCK, MR_WAVES_PER_EU) step_kernel(Dev D
     const bool run = x.code == RUN;
     if (__ballot(run) == 0) break;
     if (run && need) {  // next event: min over tester wake-up, node timers, earliest message
-      key = ((uint64_t)CS(CS_TWAKE) << 32) | (2ull << 30);
+      key = ((uint64_t)x.twake << 32) | (2ull << 30);
       cls = CLS_TESTER;
 #pragma unroll
       for (uint32_t d = 0; d < MR_MAX_NODES; d++) {  // timers of absent nodes are INF_T
         uint64_t kt = ((uint64_t)x.timer[d] << 32) | (1ull << 30) | d;
         if (kt < key) { key = kt; cls = CLS_TIMER; node = d; }
       }
-      if (x.mmin < key) { key = x.mmin; cls = CLS_MSG; }
+      if (x.mmin < key) { key = x.mmin; cls = CLS_MSG; node = (uint32_t)key & 7u; }
       need = false;
     }
     // wave-uniform choice of the event class processed this iteration
@@ -858,7 +907,7 @@ __global__ void __launch_bounds__(STEP_BLOCK, MR_WAVES_PER_EU) step_kernel(Dev D
     if (x.events > D.max_events) { fail(D, x, MR_FAIL_SIM_EVENT_LIMIT); continue; }
     if (cls != CLS_TESTER) {
       CADD(cls == CLS_MSG ? CNT_EV_MSG : CNT_EV_TIMER, 1u);
-      node_event(D, x, cls == CLS_MSG, node, x.mslot, (uint32_t)key & 0x3FFFFFFFu);
+      node_event(D, x, cls == CLS_MSG, node, x.mslot, ((uint32_t)key & 0x3FFFFFFFu) >> 3);
     } else {
       CADD(CNT_EV_TESTER, 1u);
       tester<S>(D, x);
@@ -879,7 +928,7 @@ __global__ void __launch_bounds__(STEP_BLOCK, MR_WAVES_PER_EU) step_kernel(Dev D
   CS(CS_NOW) = x.now; CS(CS_EVENTS) = x.events; CS(CS_MSGS) = x.msgs_sent;
   CS(CS_INFLIGHT) = x.inflight; CS(CS_TRACEN) = x.trace_n; CS(CS_MSLOT) = x.mslot;
   CS(CS_NETMODE) = x.netmode; CS(CS_TCTR) = x.t_ctr;
-  CS(CS_CONN) = x.conn; CS(CS_ALIVE) = x.alive;
+  CS(CS_CONN) = x.conn; CS(CS_ALIVE) = x.alive; CS(CS_TWAKE) = x.twake;
 #pragma unroll
   for (uint32_t d = 0; d < MR_MAX_NODES; d++)
     if (d < D.n) ND(NF_TIMER, d) = x.timer[d];
@@ -969,8 +1018,9 @@ hipError_t launch_reduce(const Dev& D, unsigned long long* out, uint64_t cluster
 template <uint32_t S>
 hipError_t launch_step_t(const Dev& D, uint32_t budget, hipStream_t s) {
   dim3 blk(STEP_BLOCK), grd((D.C + STEP_BLOCK - 1) / STEP_BLOCK);
-  hipLaunchKernelGGL(step_kernel<S>, grd, blk, (size_t)D.M * STEP_BLOCK * sizeof(uint64_t), s, D,
-                     budget);
+  const size_t lds = (size_t)D.M * STEP_BLOCK * sizeof(uint64_t) +  // message keys
+                    2 * MR_MAX_NODES * STEP_BLOCK * sizeof(uint32_t);  // send-loop staging
+  hipLaunchKernelGGL(step_kernel<S>, grd, blk, lds, s, D, budget);
   return hipGetLastError();
 }
 // Step-kernel instances built by this translation unit: build.py compiles

@@ -190,7 +190,7 @@ static void net_send(OSim* s, uint32_t src, uint32_t dst, OMsg* m) {
   if (!s->nd[src].conn || !s->nd[dst].conn) { s->r.drop_clog++; return; }
   if (w[0] < s->loss) { s->r.drop_loss++; return; }
   if (s->inflight >= s->cfg.msg_slots) { s->r.drop_overflow++; return; }
-  if (seq >= (1u << 30)) t_fail(s, MR_FAIL_SIM_CAPACITY);
+  if (seq >= (1u << 27)) t_fail(s, MR_FAIL_SIM_CAPACITY); /* SEMANTICS §3 */
   m->time = s->now + u_range(w[1], s->lat_lo, s->lat_hi);
   m->seq = seq; m->src = (uint8_t)src; m->dst = (uint8_t)dst;
   uint32_t slot = s->free_stack[--s->n_free];
