@@ -1,15 +1,18 @@
 // mr_dev.h — device state layout shared by the HIP kernels (mr_kernel.hip)
 // and the C++ batch driver (mr_host.cpp).
 //
-// Layout: one lane simulates one cluster. State is grouped into a few
-// field-indexed matrices, each [field][...][cluster] (cluster-minor), so the
-// 64 lanes of a wave — 64 consecutive clusters — touch 64 consecutive words
-// of a field (one or two 256-B segments per wave instruction), and the
-// kernel needs one base pointer per matrix instead of one per field (the
-// per-field pointers alone overflowed the 102-SGPR budget). Index math is
-// 32-bit (checked at batch creation). Data a lane walks by index — Raft log
-// rings, message payloads, the tester's apply checker — is cluster-major so
-// each lane's walk stays in its own cache lines (64-bit offsets).
+// Layout: one lane simulates one cluster. Two kinds of arrays:
+//  * cluster-minor matrices [field][...][C] for what every lane of a wave
+//    touches at the same field index (cluster scalars, tester frame, message
+//    keys in the launch prologue / epilogue): 64 lanes read 64 consecutive
+//    words;
+//  * cluster-major records for what a lane touches at a per-lane index — a
+//    node (the event's destination differs per lane), a message slot, log
+//    entries, apply-checker indices: one node's whole state is one 128-B
+//    record (scalars + next[] + match[]), one message one 32-B record, so an
+//    event touches one or two lines per object instead of one line per field
+//    (a [field][node][C] layout costs a line per field per lane once the
+//    lanes' node indices differ).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -45,22 +48,32 @@ enum : uint32_t {
 };
 // cs64 [C64__N][C]: per-cluster u64 scalars
 enum : uint32_t { C64_FREE, C64_DIGEST, C64_MMIN, C64_THV, C64_TV, C64__N = C64_TV + T_NV };
-// nd32 [NF__N][n][C]: per-node u32 fields
+// nd32 [C][n][NREC]: one 128-B record per node. Words 0..10 are the scalars
+// an event loads / stores as a block (load_node), 11..13 the rest, 14..15 the
+// snapshot value (u64), 16..23 next[p], 24..31 match[p] (leader -> peer p).
 enum : uint32_t {
-  NF_FLAGS, NF_TERM, NF_COMMIT, NF_APPLIED, NF_LAST, NF_SNAP, NF_SNAPT, NF_TIMER, NF_ECTR,
-  NF_NCTR, NF_SLEN, NF_PEXP, NF_PLO, NF_PHI, NF__N
+  NF_FLAGS, NF_TERM, NF_COMMIT, NF_APPLIED, NF_LAST, NF_SNAP, NF_SNAPT, NF_ECTR, NF_NCTR,
+  NF_PEXP, NF_SLEN, NF_TIMER, NF_PLO, NF_PHI, NF_SNAPV, NF__N = 16
 };
-// pr32 [PF__N][n][n][C]: leader -> peer
 enum : uint32_t { PF_NEXT, PF_MATCH, PF__N };
-// ms32 [MF__N][M][C]: in-flight message fields; ms64 [2][M][C]: key, value
-enum : uint32_t { MF_HDR, MF_TERM, MF_A, MF_B, MF_C, MF__N };
-enum : uint32_t { M64_KEY, M64_V, M64__N };
+constexpr uint32_t NR_PEER = 16;  // next[] at 16, match[] at 16 + MR_MAX_NODES
+constexpr uint32_t NREC = 32;
+// ms32 [C][M][MREC]: one 32-B record per in-flight message (value at 6..7);
+// mkey [M][C]: message keys (time, seq, dst), cluster-minor
+enum : uint32_t { MF_HDR, MF_TERM, MF_A, MF_B, MF_C, MF_PAD, MF_V, MREC = 8 };
 
 // one Raft log entry (raft.rs Log: term + command), 16 B so an entry moves as
 // one 128-bit access; message payloads (AppendEntries entries) use the same form
 struct alignas(16) LE {
   uint32_t term, pad;
   uint64_t val;
+};
+
+// one tester apply-checker index (StorageHandle, tester.rs:366-428): the value
+// the first applier stored and the mask of servers whose log holds it
+struct alignas(16) SE {
+  uint64_t val;
+  uint32_t mask, pad;
 };
 
 // ---- everything the kernels see (passed by value as a kernel argument)
@@ -71,15 +84,12 @@ struct Dev {
   uint64_t seed0;  // seed of cluster 0 = seed_base + cluster_base
   uint32_t* cs32;
   uint64_t* cs64;
-  uint32_t* nd32;
-  uint64_t* nsnapv;  // [n][C]
-  uint32_t* pr32;
-  uint32_t* ms32;
-  uint64_t* ms64;
+  uint32_t* nd32;   // [C][n][NREC]
+  uint32_t* ms32;   // [C][M][MREC]
+  uint64_t* mkey;   // [M][C]
   LE* log;  // [C][n][log_cap] ring per node
   LE* pay;  // [C][M][K] AppendEntries payload per message slot
-  uint8_t* smask;   // [C][apply_cap]   tester storage (tester.rs:366-428)
-  uint64_t* sval;
+  SE* stor;         // [C][apply_cap]   tester storage (tester.rs:366-428)
   mr_event* trace;  // [trace_clusters][trace_cap]
   uint32_t* remaining;  // clusters without verdict after a step launch
   unsigned long long* prof;  // [PROF_SLOTS] wave-cycle profile (MR_PROF builds only)

@@ -202,22 +202,18 @@ int mr_batch_create(const mr_cfg* cfg, mr_batch** out) {
   };
   // field matrices use 32-bit element offsets in the kernels
   const uint64_t lim = 1ull << 32;
-  if ((uint64_t)CS__N * C >= lim || (uint64_t)C64__N * C >= lim || NF__N * n * C >= lim ||
-      PF__N * n * n * C >= lim || MF__N * M * C >= lim || M64__N * M * C >= lim) {
+  if ((uint64_t)CS__N * C >= lim || (uint64_t)C64__N * C >= lim || M * C >= lim) {
     delete b;
     return set_err("n_clusters too large for one batch (32-bit field offsets)");
   }
   add(&D.cs32, (size_t)CS__N * C);
   add(&D.cs64, (size_t)C64__N * C);
-  add(&D.nd32, (size_t)NF__N * n * C);
-  add(&D.nsnapv, n * C);
-  add(&D.pr32, (size_t)PF__N * n * n * C);
-  add(&D.ms32, (size_t)MF__N * M * C);
-  add(&D.ms64, (size_t)M64__N * M * C);
+  add(&D.nd32, (size_t)NREC * n * C);
+  add(&D.ms32, (size_t)MREC * M * C);
+  add(&D.mkey, (size_t)M * C);
   add(&D.log, C * n * cfg->log_cap);
   add(&D.pay, C * M * K);
-  add(&D.smask, C * cfg->apply_cap);
-  add(&D.sval, C * cfg->apply_cap);
+  add(&D.stor, C * cfg->apply_cap);
   add(&D.trace, (size_t)D.trace_clusters * D.trace_cap);
   add(&D.remaining, 1);
   add(&D.prof, PROF_SLOTS);
@@ -263,7 +259,7 @@ int mr_batch_reset(mr_batch* b, uint64_t seed_base) {
   b->cfg.seed_base = seed_base;
   b->D.seed0 = seed_base + b->cfg.cluster_base;
   HIPCHK(hipSetDevice(b->cfg.device));
-  HIPCHK(hipMemsetAsync(b->D.smask, 0, (size_t)b->D.C * b->D.apply_cap, b->stream));
+  HIPCHK(hipMemsetAsync(b->D.stor, 0, (size_t)b->D.C * b->D.apply_cap * sizeof(SE), b->stream));
   HIPCHK(launch_reset(b->D, b->stream));
   HIPCHK(hipStreamSynchronize(b->stream));
   return 0;

@@ -49,11 +49,14 @@ struct X {
 // field accessors (32-bit element offsets, checked at batch creation)
 #define CS(f) D.cs32[(uint32_t)(f) * D.C + x.c]
 #define C64(f) D.cs64[(uint32_t)(f) * D.C + x.c]
-#define ND(f, d) D.nd32[((uint32_t)(f) * D.n + (d)) * D.C + x.c]
-#define NSV(d) D.nsnapv[(uint32_t)(d) * D.C + x.c]
-#define PR(f, d, p) D.pr32[(((uint32_t)(f) * D.n + (d)) * D.n + (p)) * D.C + x.c]
-#define MS32(f, mi) D.ms32[(uint32_t)(f) * D.M * D.C + (mi)]
-#define MS64(f, mi) D.ms64[(uint32_t)(f) * D.M * D.C + (mi)]
+#define NDP(d) (D.nd32 + ((size_t)x.c * D.n + (d)) * NREC)  // node d's 128-B record
+#define ND(f, d) NDP(d)[f]
+#define NSV(d) (*reinterpret_cast<uint64_t*>(NDP(d) + NF_SNAPV))
+#define PR(f, d, p) NDP(d)[NR_PEER + (f) * MR_MAX_NODES + (p)]
+#define MSP(s) (D.ms32 + ((size_t)x.c * D.M + (s)) * MREC)  // message slot s's 32-B record
+#define MS32(f, s) MSP(s)[f]
+#define MSV(s) (*reinterpret_cast<uint64_t*>(MSP(s) + MF_V))
+#define MKEY(s) D.mkey[(size_t)(s) * D.C + x.c]
 // message keys of the lane's cluster live in LDS during a launch: [slot][lane],
 // so a wave's 64 lanes read 64 consecutive u64 (conflict-free). Free slots hold
 // ~0, so the earliest-message scan is a branch-free min over all M slots.
@@ -163,21 +166,21 @@ DI size_t logi(const Dev& D, const X& x, uint32_t d, uint32_t i) {
 // One node's scalar state, loaded into registers at the start of an event
 // (one batch of independent loads) and stored back at its end.
 struct NC {
-  uint32_t f, term, commit, applied, last, snap, snapt, ectr, nctr, pexp;
+  uint32_t f, term, commit, applied, last, snap, snapt, ectr, nctr, pexp, slen, tmem;
 };
+// words 0..11 of the node record as three 16-B accesses. Word 11 (NF_TIMER) is
+// only read in the launch prologue and written in the epilogue (timers live in
+// registers), so writing back its stale copy in between is harmless.
 DI NC load_node(const Dev& D, const X& x, uint32_t d) {
-  NC n;
-  n.f = ND(NF_FLAGS, d); n.term = ND(NF_TERM, d); n.commit = ND(NF_COMMIT, d);
-  n.applied = ND(NF_APPLIED, d); n.last = ND(NF_LAST, d); n.snap = ND(NF_SNAP, d);
-  n.snapt = ND(NF_SNAPT, d); n.ectr = ND(NF_ECTR, d); n.nctr = ND(NF_NCTR, d);
-  n.pexp = ND(NF_PEXP, d);
-  return n;
+  const uint4* p = reinterpret_cast<const uint4*>(NDP(d));
+  const uint4 a = p[0], b = p[1], c = p[2];
+  return NC{a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w, c.x, c.y, c.z, c.w};
 }
 DI void store_node(const Dev& D, const X& x, uint32_t d, const NC& n) {
-  ND(NF_FLAGS, d) = n.f; ND(NF_TERM, d) = n.term; ND(NF_COMMIT, d) = n.commit;
-  ND(NF_APPLIED, d) = n.applied; ND(NF_LAST, d) = n.last; ND(NF_SNAP, d) = n.snap;
-  ND(NF_SNAPT, d) = n.snapt; ND(NF_ECTR, d) = n.ectr; ND(NF_NCTR, d) = n.nctr;
-  ND(NF_PEXP, d) = n.pexp;
+  uint4* p = reinterpret_cast<uint4*>(NDP(d));
+  p[0] = make_uint4(n.f, n.term, n.commit, n.applied);
+  p[1] = make_uint4(n.last, n.snap, n.snapt, n.ectr);
+  p[2] = make_uint4(n.nctr, n.pexp, n.slen, n.tmem);
 }
 DI uint32_t term_at(const Dev& D, const X& x, uint32_t d, const NC& n, uint32_t i) {
   if (i == 0) return 0;
@@ -262,11 +265,10 @@ DI int net_send(const Dev& D, X& x, uint32_t src, NC& s, uint32_t dst, uint32_t 
   // key = (time, seq, dst): ordered as (time, seq) since seq is unique; dst in
   // the low bits lets a delivery load the node's state before the message body
   uint64_t key = ((uint64_t)t << 32) | (seq << 3) | dst;
-  uint32_t mi = slot * D.C + x.c;
   LK(slot) = key;
-  MS32(MF_HDR, mi) = type | (src << 3) | (dst << 6) | (inc << 9) | (k << 17);
-  MS32(MF_TERM, mi) = term; MS32(MF_A, mi) = a; MS32(MF_B, mi) = b; MS32(MF_C, mi) = c;
-  if (type == M_IS_REQ) MS64(M64_V, mi) = v;
+  uint4* mp = reinterpret_cast<uint4*>(MSP(slot));
+  mp[0] = make_uint4(type | (src << 3) | (dst << 6) | (inc << 9) | (k << 17), term, a, b);
+  mp[1] = make_uint4(c, 0u, (uint32_t)v, (uint32_t)(v >> 32));
   x.inflight++;
   CMAX(CNT_MAX_INFLIGHT, x.inflight);
   if (key < x.mmin) { x.mmin = key; x.mslot = slot; }
@@ -303,12 +305,12 @@ DI void materialize(const Dev& D, X& x, uint32_t L) {
   while (occ) {
     const uint32_t s = (uint32_t)__builtin_ctzll(occ);
     occ &= occ - 1ull;
-    const uint32_t mi = s * D.C + x.c, hdr = MS32(MF_HDR, mi), k = (hdr >> 17) & 63u;
+    const uint32_t hdr = MS32(MF_HDR, s), k = (hdr >> 17) & 63u;
     if ((hdr & 7u) != M_AE_REQ || ((hdr >> 3) & 7u) != L || (hdr & HDR_MAT) || k == 0) continue;
-    const uint32_t prev = MS32(MF_A, mi);
+    const uint32_t prev = MS32(MF_A, s);
     LE* pp = D.pay + ((size_t)x.c * D.M + s) * D.K;
     for (uint32_t j = 0; j < k; j++) pp[j] = D.log[logi(D, x, L, prev + 1 + j)];
-    MS32(MF_HDR, mi) = hdr | HDR_MAT;
+    MS32(MF_HDR, s) = hdr | HDR_MAT;
   }
   ND(NF_PLO, L) = 1u;  // empty range
   ND(NF_PHI, L) = 0u;
@@ -331,21 +333,21 @@ constexpr uint32_t AC = 4;  // entries per batch of independent loads in log wal
 #define MR_AC_APPLY 8
 #endif
 constexpr uint32_t AC_APPLY = MR_AC_APPLY;  // entries per batch in the applier
-DI void storage_snapshot(const Dev& D, X& x, uint32_t i, uint32_t idx) {  // tester.rs:399-402
+DI void storage_snapshot(const Dev& D, X& x, uint32_t i, uint32_t& slen, uint32_t idx) {  // tester.rs:399-402
   if (idx >= D.apply_cap) { fail(D, x, MR_FAIL_SIM_CAPACITY); return; }
-  uint32_t nl = idx + 1, len = ND(NF_SLEN, i);
-  for (uint32_t j = nl; j < len; j++) {
-    size_t si = (size_t)x.c * D.apply_cap + j;
-    D.smask[si] = (uint8_t)(D.smask[si] & ~(1u << i));
+  uint32_t nl = idx + 1;
+  for (uint32_t j = nl; j < slen; j++) {
+    SE* e = D.stor + (size_t)x.c * D.apply_cap + j;
+    e->mask &= ~(1u << i);
   }
-  ND(NF_SLEN, i) = nl;
+  slen = nl;
 }
 
 DI uint32_t n_committed(const Dev& D, X& x, uint32_t idx, uint64_t& v) {  // tester.rs:405-422
   if (idx >= D.apply_cap) { v = 0; return 0; }
-  size_t si = (size_t)x.c * D.apply_cap + idx;
-  v = D.sval[si];
-  return (uint32_t)__builtin_popcount((uint32_t)D.smask[si]);
+  const SE e = D.stor[(size_t)x.c * D.apply_cap + idx];
+  v = e.val;
+  return (uint32_t)__builtin_popcount(e.mask);
 }
 
 // ---------------------------------------------------------------- Raft node
@@ -366,8 +368,8 @@ enum : uint32_t { SEND_NONE = 0, SEND_REPLY, SEND_APPEND, SEND_VOTE };
 // used — entries have distinct indices, so a batch never reads what it writes.
 DI void node_apply(const Dev& D, X& x, uint32_t me, NC& d) {
   const bool snapmode = (x.netmode >> 1) & 1u;
-  const size_t sb = (size_t)x.c * D.apply_cap;
-  uint32_t len = ND(NF_SLEN, me);
+  SE* const sb = D.stor + (size_t)x.c * D.apply_cap;
+  uint32_t len = d.slen;
   while (d.applied < d.commit) {
     const uint32_t i0 = d.applied + 1;
     LE e[AC_APPLY];
@@ -378,8 +380,9 @@ DI void node_apply(const Dev& D, X& x, uint32_t me, NC& d) {
       const uint32_t i = i0 + j;
       const bool ok = i <= d.commit && i < D.apply_cap;
       e[j] = ok ? D.log[logi(D, x, me, i)] : LE{};
-      m[j] = ok ? D.smask[sb + i] : 0u;
-      sv[j] = ok ? D.sval[sb + i] : 0ull;
+      const SE s = ok ? sb[i] : SE{};
+      m[j] = s.mask;
+      sv[j] = s.val;
     }
     PROF(P_AP_LOAD);
 #pragma unroll
@@ -392,8 +395,7 @@ DI void node_apply(const Dev& D, X& x, uint32_t me, NC& d) {
       if (m[j] && sv[j] != e[j].val) { fail(D, x, MR_FAIL_APPLY_MISMATCH); return; }  // tester.rs:384
       if (i > len) { fail(D, x, MR_FAIL_APPLY_OUT_OF_ORDER); return; }  // tester.rs:393
       if (i == len) {
-        D.sval[sb + i] = e[j].val;
-        D.smask[sb + i] = (uint8_t)(m[j] | (1u << me));
+        sb[i] = SE{e[j].val, m[j] | (1u << me), 0u};
         len++;
         CMAX(CNT_MAX_INDEX, i);
       }
@@ -406,7 +408,7 @@ DI void node_apply(const Dev& D, X& x, uint32_t me, NC& d) {
     }
     PROF(P_AP_CHECK);
   }
-  ND(NF_SLEN, me) = len;
+  d.slen = len;
 }
 
 // commit = the majority-th largest of the match indices mv[] (mv[me] = last),
@@ -459,11 +461,11 @@ DI void ae_load_batch(const Dev& D, const X& x, uint32_t me, const NC& d, uint32
 DI void node_event(const Dev& D, X& x, bool is_msg, uint32_t tnode, uint32_t slot,
                    uint32_t seq) {
   uint32_t me = tnode, src = 0, type = 0, inc = 0, k = 0, mterm = 0, ma = 0, mb = 0, mc = 0;
-  uint32_t mi = 0, hdr_bits = 0;
+  uint32_t hdr_bits = 0;
   if (is_msg) {
-    mi = slot * D.C + x.c;
-    uint32_t hdr = MS32(MF_HDR, mi);
-    mterm = MS32(MF_TERM, mi); ma = MS32(MF_A, mi); mb = MS32(MF_B, mi); mc = MS32(MF_C, mi);
+    const uint4 m0 = reinterpret_cast<const uint4*>(MSP(slot))[0];
+    const uint32_t hdr = m0.x;
+    mterm = m0.y; ma = m0.z; mb = m0.w; mc = MS32(MF_C, slot);
     type = hdr & 7u; src = (hdr >> 3) & 7u; inc = (hdr >> 9) & 255u;  // dst = tnode (key)
     k = (hdr >> 17) & 63u;
     hdr_bits = hdr;
@@ -599,9 +601,9 @@ DI void node_event(const Dev& D, X& x, bool is_msg, uint32_t tnode, uint32_t slo
         uint32_t idx = ma;
         if (idx > d.commit) {
           if (!(idx <= d.last && term_at(D, x, me, d, idx) == mb)) d.last = idx;
-          d.snap = idx; d.snapt = mb; NSV(me) = MS64(M64_V, mi);
+          d.snap = idx; d.snapt = mb; NSV(me) = MSV(slot);
           d.commit = idx; d.applied = idx;
-          storage_snapshot(D, x, me, idx);
+          storage_snapshot(D, x, me, d.slen, idx);
           if (x.code != RUN) return;
           CADD(CNT_INSTALLS, 1u);
         }
@@ -862,7 +864,7 @@ __global__ void __launch_bounds__(STEP_BLOCK, MR_WAVES_PER_EU) step_kernel(Dev D
 #pragma unroll
     for (uint32_t k = 0; k < CNT__N; k++) x.cnt[k] = CS(CS_CNT + k);
 #endif
-    for (uint32_t s = 0; s < D.M; s++) LK(s) = MS64(M64_KEY, s * D.C + x.c);
+    for (uint32_t s = 0; s < D.M; s++) LK(s) = MKEY(s);
   }
   const bool live = x.code == RUN;
   PROF(P_PRO);
@@ -937,7 +939,7 @@ __global__ void __launch_bounds__(STEP_BLOCK, MR_WAVES_PER_EU) step_kernel(Dev D
 #pragma unroll
   for (uint32_t k = 0; k < CNT__N; k++) CS(CS_CNT + k) = x.cnt[k];
 #endif
-  for (uint32_t s = 0; s < D.M; s++) MS64(M64_KEY, s * D.C + x.c) = LK(s);
+  for (uint32_t s = 0; s < D.M; s++) MKEY(s) = LK(s);
   if (x.code == RUN) atomicAdd(D.remaining, 1u);
 }
 
@@ -965,7 +967,7 @@ __global__ void __launch_bounds__(256) reset_kernel(Dev D) {
     NSV(d) = 0;
     for (uint32_t p = 0; p < D.n; p++) { PR(PF_NEXT, d, p) = 0; PR(PF_MATCH, d, p) = 0; }
   }
-  for (uint32_t s = 0; s < D.M; s++) MS64(M64_KEY, s * D.C + x.c) = ~0ull;
+  for (uint32_t s = 0; s < D.M; s++) MKEY(s) = ~0ull;
 }
 
 // counters_reduce: per-GPU sums / maxima / verdict histogram / first failing
