@@ -724,10 +724,21 @@ DI void t_new(const Dev& D, X& x, bool snapshot) {  // RaftTester::new, tester.r
   for (uint32_t i = 0; i < D.n; i++) { t_start1(D, x, i); t_conn(D, x, i, 1); }
   if (D.unrel_flag) t_set_unrel(x, true);
 }
-// tester.rs:165-171 -> raft.rs:238-244; unwrap() on a crashed raft panics
-DI bool t_start(const Dev& D, X& x, uint32_t i, uint64_t v, uint32_t& idx, uint32_t& term) {
+// bit mask of the servers whose role is leader: one batch of independent loads
+// (a start() changes only its own server, so a loop of starts can use it)
+DI uint32_t t_leaders(const Dev& D, X& x) {
+  uint32_t m = 0;
+#pragma unroll
+  for (uint32_t i = 0; i < MR_MAX_NODES; i++)
+    m |= (i < D.n && f_role(ND(NF_FLAGS, i)) == R_L) ? 1u << i : 0u;
+  return m;
+}
+// tester.rs:165-171 -> raft.rs:238-244; unwrap() on a crashed raft panics.
+// `lead` = whether server i is leader (t_leaders), read before the call.
+DI bool t_start(const Dev& D, X& x, uint32_t i, uint64_t v, uint32_t& idx, uint32_t& term,
+                bool lead) {
   if (!bit(x.alive, i)) { fail(D, x, MR_FAIL_UNWRAP_NONE); return false; }
-  if (D.null_raft || f_role(ND(NF_FLAGS, i)) != R_L) return false;  // Err(NotLeader((me+1)%n))
+  if (D.null_raft || !lead) return false;  // Err(NotLeader((me+1)%n))
   uint32_t snap = ND(NF_SNAP, i), last = ND(NF_LAST, i) + 1;
   if (last - snap > D.log_cap) { fail(D, x, MR_FAIL_SIM_CAPACITY); return false; }
   size_t li = logi(D, x, i, last);
@@ -741,6 +752,9 @@ DI bool t_start(const Dev& D, X& x, uint32_t i, uint64_t v, uint32_t& idx, uint3
   PR(PF_MATCH, i, i) = last;
   idx = last;
   return true;
+}
+DI bool t_start(const Dev& D, X& x, uint32_t i, uint64_t v, uint32_t& idx, uint32_t& term) {
+  return t_start(D, x, i, v, idx, term, f_role(ND(NF_FLAGS, i)) == R_L);
 }
 DI bool t_start(const Dev& D, X& x, uint32_t i, uint64_t v) {
   uint32_t a, b;
