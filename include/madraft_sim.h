@@ -68,6 +68,10 @@ enum mr_scenario {
   /* BASELINE.json config 3 read literally: figure_8_unreliable_2c's loop with
    * crash1/start1 (figure_8_2c, tests.rs:638-649) in place of disconnect. */
   MR_SCN_FIGURE_8_UNRELIABLE_CRASH = 24,
+  /* kvraft generic_test (src/kvraft/tests.rs:65-220) over 5 servers; BASELINE config 5 */
+  MR_SCN_KV_BASIC_3A = 25,               /* kvraft/tests.rs:222-226: 1 client        */
+  MR_SCN_KV_CONCURRENT_3A = 26,          /* kvraft/tests.rs:228-232: 5 clients       */
+  MR_SCN_KV_UNRELIABLE_3A = 27,          /* kvraft/tests.rs:234-238: 5, unreliable   */
   MR_SCN_COUNT_
 };
 
@@ -105,6 +109,9 @@ enum mr_fail {
   MR_FAIL_RPC_TOO_MANY = 24,      /* tests.rs:462 "too many RPCs ({}) for {} entries" */
   MR_FAIL_RPC_IDLE = 25,          /* tests.rs:472-476 "too many RPCs for 1 second of idleness" */
   MR_FAIL_CHURN_VALUE = 26,       /* tests.rs:852 "didn't find a value" */
+  MR_FAIL_KV_GET_WRONG = 27,      /* kvraft/tests.rs:127 "get wrong value, key {:?}" */
+  MR_FAIL_KV_MISSING = 28,        /* kvraft/tests.rs:25-30 "missing element {:?} in Append result" */
+  MR_FAIL_KV_APPEND_BAD = 29,     /* kvraft/tests.rs:31-39 duplicate / wrong order element */
   /* simulator limits (not reference panics): a cluster that hits one is reported, never passed */
   MR_FAIL_SIM_CAPACITY = 60,      /* a log / apply / sequence capacity of the config was exceeded */
   MR_FAIL_SIM_EVENT_LIMIT = 61,   /* cfg.max_events processed without a verdict */

@@ -26,11 +26,15 @@ SCENARIOS = [
     "unreliable_agree_2c", "figure_8_unreliable_2c", "reliable_churn_2c",
     "unreliable_churn_2c", "snapshot_basic_2d", "snapshot_install_2d",
     "snapshot_install_unreliable_2d", "snapshot_install_crash_2d",
-    "snapshot_install_unreliable_crash_2d", "figure_8_unreliable_crash",
+    "snapshot_install_unreliable_crash_2d", "figure_8_unreliable_crash", "basic_3a",
+    "concurrent_3a", "unreliable_3a",
 ]
 SCENARIO_ID = {n: i for i, n in enumerate(SCENARIOS) if n}
 # tests that still need multi-threaded tester programs (spawn_local); not built yet
 UNSUPPORTED = {"unreliable_agree_2c", "reliable_churn_2c", "unreliable_churn_2c"}
+# kvraft generic_test (src/kvraft/tests.rs); oracle-only until the HIP path lands
+KV_TESTS = ["basic_3a", "concurrent_3a", "unreliable_3a"]
+GPU_UNSUPPORTED = UNSUPPORTED | set(KV_TESTS)
 
 FAIL_NAMES = {
     0: "PASS", 1: "ONE_LEADER_NONE", 2: "MULTI_LEADER_TERM", 3: "TERM_DISAGREE",
@@ -39,7 +43,8 @@ FAIL_NAMES = {
     12: "LOG_SIZE", 13: "BASIC_PRECOMMIT", 14: "BASIC_INDEX", 15: "LEADER_REJECTED",
     16: "EXPECTED_INDEX2", 17: "NO_MAJORITY_COMMIT", 18: "UNEXPECTED_INDEX", 19: "CMD_MISSING",
     20: "TERM_CHANGED", 21: "RPC_INITIAL", 22: "START_FAILED", 23: "WRONG_VALUE",
-    24: "RPC_TOO_MANY", 25: "RPC_IDLE", 26: "CHURN_VALUE", 60: "SIM_CAPACITY",
+    24: "RPC_TOO_MANY", 25: "RPC_IDLE", 26: "CHURN_VALUE", 27: "KV_GET_WRONG", 28: "KV_MISSING",
+    29: "KV_APPEND_BAD", 60: "SIM_CAPACITY",
     61: "SIM_EVENT_LIMIT", 62: "SIM_BAD_PROGRAM", 0xFFFF: "RUNNING",
 }
 

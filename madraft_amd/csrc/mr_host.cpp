@@ -53,10 +53,11 @@ const char* k_names[MR_SCN_COUNT_] = {
     "unreliable_agree_2c", "figure_8_unreliable_2c", "reliable_churn_2c",
     "unreliable_churn_2c", "snapshot_basic_2d", "snapshot_install_2d",
     "snapshot_install_unreliable_2d", "snapshot_install_crash_2d",
-    "snapshot_install_unreliable_crash_2d", "figure_8_unreliable_crash"};
+    "snapshot_install_unreliable_crash_2d", "figure_8_unreliable_crash", "basic_3a",
+    "concurrent_3a", "unreliable_3a"};
 // servers per test (tests.rs `let servers = ..`)
 const uint8_t k_nodes[MR_SCN_COUNT_] = {0, 3, 3, 7, 5, 3, 5, 3, 3, 5, 3, 3, 5, 3,
-                                        5, 5, 5, 5, 5, 3, 3, 3, 3, 3, 5};
+                                        5, 5, 5, 5, 5, 3, 3, 3, 3, 3, 5, 5, 5, 5};
 
 constexpr size_t RED_N = CNT__N + 8 + 64;  // reduce_kernel output slots
 }  // namespace
@@ -115,6 +116,9 @@ const char* mr_fail_message(uint32_t code) {
     case MR_FAIL_RPC_TOO_MANY: return "too many RPCs for entries";
     case MR_FAIL_RPC_IDLE: return "too many RPCs for 1 second of idleness";
     case MR_FAIL_CHURN_VALUE: return "didn't find a value";
+    case MR_FAIL_KV_GET_WRONG: return "get wrong value";
+    case MR_FAIL_KV_MISSING: return "missing element in Append result";
+    case MR_FAIL_KV_APPEND_BAD: return "duplicate or wrong order element in Append result";
     case MR_FAIL_SIM_CAPACITY: return "simulator capacity exceeded";
     case MR_FAIL_SIM_EVENT_LIMIT: return "simulator event limit exceeded";
     case MR_FAIL_SIM_BAD_PROGRAM: return "scenario program error";
@@ -136,9 +140,11 @@ int mr_cfg_init(mr_cfg* c, uint32_t scn) {
   int fig8 = scn == MR_SCN_FIGURE_8_2C || scn == MR_SCN_FIGURE_8_UNRELIABLE_2C ||
              scn == MR_SCN_FIGURE_8_UNRELIABLE_CRASH;
   int snap = scn >= MR_SCN_SNAPSHOT_BASIC_2D && scn <= MR_SCN_SNAPSHOT_INSTALL_UNRELIABLE_CRASH_2D;
-  c->log_cap = fig8 ? 2048 : 256;
-  c->apply_cap = fig8 ? 2048 : (snap ? 1024 : 512);
-  c->msg_slots = 32;
+  int kv = scn >= MR_SCN_KV_BASIC_3A && scn <= MR_SCN_KV_UNRELIABLE_3A;
+  uint32_t kvcap = scn == MR_SCN_KV_CONCURRENT_3A ? 8192 : 2048;
+  c->log_cap = fig8 ? 2048 : (kv ? kvcap : 256);
+  c->apply_cap = fig8 ? 2048 : (snap ? 1024 : (kv ? kvcap : 512));
+  c->msg_slots = kv ? 64 : 32;
   c->ae_max = 16;
   c->hb_us = 50000;
   c->elect_lo_us = 150000;  // raft.rs:262
@@ -171,7 +177,7 @@ int mr_batch_create(const mr_cfg* cfg, mr_batch** out) {
   if (validate(cfg) != 0) return -1;
   const uint32_t scn = cfg->scenario;
   if (scn == MR_SCN_UNRELIABLE_AGREE_2C || scn == MR_SCN_RELIABLE_CHURN_2C ||
-      scn == MR_SCN_UNRELIABLE_CHURN_2C)
+      scn == MR_SCN_UNRELIABLE_CHURN_2C || scn >= MR_SCN_KV_BASIC_3A)
     return set_err(std::string("scenario needs concurrent tester tasks (not built yet): ") +
                    k_names[scn]);
 

@@ -188,6 +188,16 @@ DI uint32_t term_at(const Dev& D, const X& x, uint32_t d, const NC& n, uint32_t 
   return D.log[logi(D, x, d, i)].term;
 }
 
+// message header word: type[0:4) src[4:9) dst[9:14) inc/tag[14:22) k[22:28) MAT[28]
+// (hosts: servers 0..7, clerks 8..31)
+DI uint32_t hdr_make(uint32_t type, uint32_t src, uint32_t dst, uint32_t inc, uint32_t k) {
+  return type | (src << 4) | (dst << 9) | ((inc & 255u) << 14) | (k << 22);
+}
+DI uint32_t hdr_type(uint32_t h) { return h & 15u; }
+DI uint32_t hdr_src(uint32_t h) { return (h >> 4) & 31u; }
+DI uint32_t hdr_inc(uint32_t h) { return (h >> 14) & 255u; }
+DI uint32_t hdr_k(uint32_t h) { return (h >> 22) & 63u; }
+
 DI uint32_t net_loss(const X& x) { return (x.netmode & 1u) ? LOSS_Q32 : 0u; }  // tester.rs:127-137
 DI uint32_t net_lat_hi(const X& x) { return (x.netmode & 1u) ? 27000u : 10000u; }
 
@@ -258,16 +268,16 @@ DI int net_send(const Dev& D, X& x, uint32_t src, NC& s, uint32_t dst, uint32_t 
   philox(D, x, ctr, src, ST_NET, w0, w1);
   if (w0 < net_loss(x)) { CADD(CNT_DROP_LOSS, 1u); return -1; }
   if (x.inflight >= D.M) { CADD(CNT_DROP_OVERFLOW, 1u); return -1; }
-  if (seq >= (1u << 27)) { fail(D, x, MR_FAIL_SIM_CAPACITY); return -1; }  // SEMANTICS §3
+  if (seq >= (1u << 25)) { fail(D, x, MR_FAIL_SIM_CAPACITY); return -1; }  // SEMANTICS §3, §9
   uint32_t t = x.now + u_range(w1, 1000u, net_lat_hi(x));
   uint32_t slot = (uint32_t)__builtin_ctzll(x.free_mask);
   x.free_mask &= ~(1ull << slot);
-  // key = (time, seq, dst): ordered as (time, seq) since seq is unique; dst in
-  // the low bits lets a delivery load the node's state before the message body
-  uint64_t key = ((uint64_t)t << 32) | (seq << 3) | dst;
+  // key = (time, seq, dst): ordered as (time, seq) since seq is unique; dst (5
+  // bits) in the low bits lets a delivery load the node's state before the message body
+  uint64_t key = ((uint64_t)t << 32) | (seq << 5) | dst;
   LK(slot) = key;
   uint4* mp = reinterpret_cast<uint4*>(MSP(slot));
-  mp[0] = make_uint4(type | (src << 3) | (dst << 6) | (inc << 9) | (k << 17), term, a, b);
+  mp[0] = make_uint4(hdr_make(type, src, dst, inc, k), term, a, b);
   mp[1] = make_uint4(c, 0u, (uint32_t)v, (uint32_t)(v >> 32));
   x.inflight++;
   CMAX(CNT_MAX_INFLIGHT, x.inflight);
@@ -285,7 +295,7 @@ DI int net_send(const Dev& D, X& x, uint32_t src, NC& s, uint32_t dst, uint32_t 
 // referenced slot first materializes (copies) those messages' payloads into
 // their slots — rare: it takes a deposed leader whose entries are replaced, or
 // a ring that wraps under in-flight messages.
-constexpr uint32_t HDR_MAT = 1u << 23;  // message header: payload copied into D.pay
+constexpr uint32_t HDR_MAT = 1u << 28;  // message header: payload copied into D.pay
 constexpr uint32_t LAT_BOUND_US = 27000u;
 
 DI void pend_note(const Dev& D, X& x, uint32_t me, NC& d, uint32_t lo, uint32_t hi) {
@@ -305,8 +315,8 @@ DI void materialize(const Dev& D, X& x, uint32_t L) {
   while (occ) {
     const uint32_t s = (uint32_t)__builtin_ctzll(occ);
     occ &= occ - 1ull;
-    const uint32_t hdr = MS32(MF_HDR, s), k = (hdr >> 17) & 63u;
-    if ((hdr & 7u) != M_AE_REQ || ((hdr >> 3) & 7u) != L || (hdr & HDR_MAT) || k == 0) continue;
+    const uint32_t hdr = MS32(MF_HDR, s), k = hdr_k(hdr);
+    if (hdr_type(hdr) != M_AE_REQ || hdr_src(hdr) != L || (hdr & HDR_MAT) || k == 0) continue;
     const uint32_t prev = MS32(MF_A, s);
     LE* pp = D.pay + ((size_t)x.c * D.M + s) * D.K;
     for (uint32_t j = 0; j < k; j++) pp[j] = D.log[logi(D, x, L, prev + 1 + j)];
@@ -466,8 +476,8 @@ DI void node_event(const Dev& D, X& x, bool is_msg, uint32_t tnode, uint32_t slo
     const uint4 m0 = reinterpret_cast<const uint4*>(MSP(slot))[0];
     const uint32_t hdr = m0.x;
     mterm = m0.y; ma = m0.z; mb = m0.w; mc = MS32(MF_C, slot);
-    type = hdr & 7u; src = (hdr >> 3) & 7u; inc = (hdr >> 9) & 255u;  // dst = tnode (key)
-    k = (hdr >> 17) & 63u;
+    type = hdr_type(hdr); src = hdr_src(hdr); inc = hdr_inc(hdr);  // dst = tnode (key)
+    k = hdr_k(hdr);
     hdr_bits = hdr;
     LK(slot) = ~0ull;
     x.free_mask |= 1ull << slot;
@@ -898,7 +908,7 @@ __global__ void __launch_bounds__(STEP_BLOCK, MR_WAVES_PER_EU) step_kernel(Dev D
         uint64_t kt = ((uint64_t)x.timer[d] << 32) | (1ull << 30) | d;
         if (kt < key) { key = kt; cls = CLS_TIMER; node = d; }
       }
-      if (x.mmin < key) { key = x.mmin; cls = CLS_MSG; node = (uint32_t)key & 7u; }
+      if (x.mmin < key) { key = x.mmin; cls = CLS_MSG; node = (uint32_t)key & 31u; }
       need = false;
     }
     // wave-uniform choice of the event class processed this iteration
@@ -923,7 +933,7 @@ __global__ void __launch_bounds__(STEP_BLOCK, MR_WAVES_PER_EU) step_kernel(Dev D
     if (x.events > D.max_events) { fail(D, x, MR_FAIL_SIM_EVENT_LIMIT); continue; }
     if (cls != CLS_TESTER) {
       CADD(cls == CLS_MSG ? CNT_EV_MSG : CNT_EV_TIMER, 1u);
-      node_event(D, x, cls == CLS_MSG, node, x.mslot, ((uint32_t)key & 0x3FFFFFFFu) >> 3);
+      node_event(D, x, cls == CLS_MSG, node, x.mslot, ((uint32_t)key & 0x3FFFFFFFu) >> 5);
     } else {
       CADD(CNT_EV_TESTER, 1u);
       tester<S>(D, x);

@@ -39,7 +39,13 @@ void mro_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2], uint32_t ou
 
 enum { ST_TESTER = 1, ST_ELECT = 2, ST_NET = 3 };
 enum { R_F = 0, R_C = 1, R_L = 2, R_DOWN = 3 };
-enum { M_RV_REQ = 1, M_RV_REP, M_AE_REQ, M_AE_REP, M_IS_REQ, M_IS_REP };
+enum { M_RV_REQ = 1, M_RV_REP, M_AE_REQ, M_AE_REP, M_IS_REQ, M_IS_REP, M_KV_REQ, M_KV_REP };
+enum { KV_GET = 0, KV_PUT = 1, KV_APPEND = 2 };
+enum { KV_OK = 0, KV_WRONG_LEADER = 1, KV_FAILED = 2 };
+#define CLERK_HOST 8u   /* clerk c is host 8 + c (SEMANTICS §9) */
+#define MAX_CLERKS 16u
+#define KV_SLOTS 6u     /* thread / clerk slots: 0 = main + ck, 1 + cli = client cli */
+#define KV_PEND 8u
 #define INF_T 0xFFFFFFFFu
 #define LOSS_Q32 429496729u /* floor(0.1 * 2^32), tester.rs:130 */
 
@@ -70,6 +76,16 @@ typedef struct {
 
 typedef struct { uint64_t key; uint32_t ref; uint32_t gen; } HEnt;
 
+/* kvraft clerk (kvraft/client.rs ClerkCore) and the tester thread that owns it */
+typedef struct {
+  uint32_t id, lh, seq, tag, nctr, waiting, got, rstat, rhint, rval;
+  uint32_t op, key, elem;
+} OClerk;
+typedef struct {
+  uint32_t tid, live, pc, j, cli, tctr, gen, done_at;
+} OThr;
+typedef struct { uint32_t used, idx, clerk, seq, tag, ready, status, value; } OPend;
+
 typedef struct {
   mr_cfg cfg;
   uint32_t n, key[2], now, scenario, snapshot_mode, null_raft;
@@ -82,6 +98,11 @@ typedef struct {
   /* tester */
   uint32_t t_ctr;
   uint8_t* mask; uint64_t* sval; uint32_t slen[MR_MAX_NODES];
+  /* kvraft (SEMANTICS §8-9) */
+  uint32_t kv_mode, kv_done, next_tid, mwake, main_join;
+  uint32_t kv_n[MR_MAX_NODES][8], kv_ok[MR_MAX_NODES], kv_dedup[MR_MAX_NODES][MAX_CLERKS];
+  OPend pend[MR_MAX_NODES][KV_PEND];
+  OClerk ck[KV_SLOTS]; OThr th[KV_SLOTS];
   /* results */
   mro_result r;
   mr_event* trace; size_t trace_cap, n_trace;
@@ -181,16 +202,24 @@ static void reset_timer(OSim* s, uint32_t d) {
 /* ------------------------------------------------------------------ */
 /* network (madsim net: tester.rs:127-137 config, :147-149 stat)        */
 /* ------------------------------------------------------------------ */
+static int host_conn(OSim* s, uint32_t h) { return h < CLERK_HOST ? s->nd[h].conn : 1; }
+static uint32_t* host_nctr(OSim* s, uint32_t h) {
+  if (h < CLERK_HOST) return &s->nd[h].n_ctr;
+  for (uint32_t k = 0; k < KV_SLOTS; k++)
+    if (s->ck[k].id == h - CLERK_HOST) return &s->ck[k].nctr;
+  t_fail(s, MR_FAIL_SIM_BAD_PROGRAM);
+  return NULL;
+}
+
 static void net_send(OSim* s, uint32_t src, uint32_t dst, OMsg* m) {
   uint32_t seq = (uint32_t)s->r.msgs_sent;
   s->r.msgs_sent++;
-  ONode* x = &s->nd[src];
-  uint32_t ctr[4] = {x->n_ctr++, src, ST_NET, 0}, w[4];
+  uint32_t ctr[4] = {(*host_nctr(s, src))++, src, ST_NET, 0}, w[4];
   mro_philox4x32_10(ctr, s->key, w);
-  if (!s->nd[src].conn || !s->nd[dst].conn) { s->r.drop_clog++; return; }
+  if (!host_conn(s, src) || !host_conn(s, dst)) { s->r.drop_clog++; return; }
   if (w[0] < s->loss) { s->r.drop_loss++; return; }
   if (s->inflight >= s->cfg.msg_slots) { s->r.drop_overflow++; return; }
-  if (seq >= (1u << 27)) t_fail(s, MR_FAIL_SIM_CAPACITY); /* SEMANTICS §3 */
+  if (seq >= (1u << 25)) t_fail(s, MR_FAIL_SIM_CAPACITY); /* SEMANTICS §3, §9 */
   m->time = s->now + u_range(w[1], s->lat_lo, s->lat_hi);
   m->seq = seq; m->src = (uint8_t)src; m->dst = (uint8_t)dst;
   uint32_t slot = s->free_stack[--s->n_free];
@@ -248,6 +277,47 @@ static void log_put(OSim* s, ONode* d, uint32_t i, uint32_t t, uint64_t v) {
   if (i - d->snap_idx > s->r.max_log) s->r.max_log = i - d->snap_idx;
 }
 
+/* kvraft Server::apply + Kv::apply (the build's completion of kvraft/server.rs:68-87,
+ * SEMANTICS §9): dedup by (clerk, seq), value model (n, ok), answer pending requests */
+static void kv_apply(OSim* s, uint32_t me, uint32_t i, uint64_t v) {
+  uint32_t op = (uint32_t)(v >> 56) & 3u, key = (uint32_t)(v >> 53) & 7u;
+  uint32_t clerk = (uint32_t)(v >> 48) & 31u, seq = (uint32_t)(v >> 24) & 0xFFFFFFu;
+  uint32_t elem = (uint32_t)v & 0xFFFFFFu, out = 0;
+  uint32_t* n = &s->kv_n[me][key];
+  if (op == KV_GET) {
+    out = *n | (((s->kv_ok[me] >> key) & 1u) << 31);
+  } else if (seq > s->kv_dedup[me][clerk]) {
+    if (op == KV_PUT) { *n = 0; s->kv_ok[me] |= 1u << key; }
+    else if (((s->kv_ok[me] >> key) & 1u) && elem == *n) (*n)++;
+    else s->kv_ok[me] &= ~(1u << key);
+    s->kv_dedup[me][clerk] = seq;
+  }
+  for (uint32_t p = 0; p < KV_PEND; p++) { /* answered at the end of the event (kv_flush) */
+    OPend* q = &s->pend[me][p];
+    if (!q->used || q->ready || q->idx != i) continue;
+    int ok = q->clerk == clerk && q->seq == seq;
+    q->ready = 1; q->status = ok ? KV_OK : KV_FAILED; q->value = (ok && op == KV_GET) ? out : 0;
+  }
+}
+
+static void kv_send_rep(OSim* s, uint32_t src, uint32_t dst, uint32_t tag, uint32_t status,
+                        uint32_t hint, uint32_t value) {
+  OMsg m;
+  m.type = M_KV_REP; m.inc = 0; m.term = tag; m.a = status; m.b = hint; m.c = value;
+  m.k = 0; m.v = 0;
+  net_send(s, src, dst, &m);
+}
+
+/* the event's answered requests at server me, after its Raft sends, in slot order (SEMANTICS §9) */
+static void kv_flush(OSim* s, uint32_t me) {
+  for (uint32_t p = 0; p < KV_PEND; p++) {
+    OPend* q = &s->pend[me][p];
+    if (!q->used || !q->ready) continue;
+    q->used = 0; q->ready = 0;
+    kv_send_rep(s, me, CLERK_HOST + q->clerk, q->tag, q->status, 0, q->value);
+  }
+}
+
 /* tester.rs:303-325 applier: push_and_check, snapshot every SNAPSHOT_INTERVAL */
 static void node_apply(OSim* s, uint32_t me) {
   ONode* d = &s->nd[me];
@@ -255,6 +325,7 @@ static void node_apply(OSim* s, uint32_t me) {
     uint32_t i = ++d->applied;
     uint64_t v = d->lval[lpos(s, i)];
     push_and_check(s, me, i, v);
+    if (s->kv_mode) kv_apply(s, me, i, v);
     if (s->snapshot_mode && (i + 1) % 10 == 0 && i > d->snap_idx) {
       d->snap_term = term_at(s, d, i);
       d->snap_val = v;
@@ -328,10 +399,57 @@ static void reply(OSim* s, uint32_t me, const OMsg* req, uint32_t type, uint32_t
   net_send(s, me, req->src, &m);
 }
 
+static void rec_host(OSim* s, uint32_t kind, uint32_t host, uint32_t aux) {
+  mr_event e;
+  memset(&e, 0, sizeof e);
+  e.time_us = s->now; e.cls = 0; e.kind = (uint8_t)kind; e.node = (uint8_t)host; e.aux = aux;
+  rec_push(s, &e);
+}
+
+static void thr_wake(OSim* s, uint32_t slot, uint32_t t);
+
+/* KV_REP at a clerk host: wake the clerk's thread if it waits for this tag */
+static void clerk_deliver(OSim* s, OMsg* m) {
+  uint32_t id = m->dst - CLERK_HOST;
+  OClerk* c = NULL;
+  uint32_t slot = 0;
+  for (uint32_t k = 0; k < KV_SLOTS; k++)
+    if (s->th[k].live && s->ck[k].id == id) { c = &s->ck[k]; slot = k; }
+  if (!host_conn(s, m->src)) { s->r.drop_deliver++; rec_host(s, 16, m->dst, m->seq); return; }
+  if (!c || !c->waiting || c->got || m->term != c->tag) {
+    s->r.drop_stale++;
+    rec_host(s, 17, m->dst, m->seq);
+    return;
+  }
+  c->got = 1; c->rstat = m->a; c->rhint = m->b; c->rval = m->c;
+  thr_wake(s, slot, s->now);
+  rec_host(s, M_KV_REP, m->dst, m->seq);
+}
+
+/* KV_REQ at server `me` (kvraft/server.rs:48-56 handler + :68-70 apply, SEMANTICS §9) */
+static void kv_request(OSim* s, uint32_t me, OMsg* m) {
+  ONode* d = &s->nd[me];
+  uint32_t clerk = m->src - CLERK_HOST;
+  if (s->null_raft || d->role != R_L) {
+    kv_send_rep(s, me, m->src, m->term, KV_WRONG_LEADER, (me + 1) % s->n, 0);
+    return;
+  }
+  uint32_t p = 0;
+  while (p < KV_PEND && s->pend[me][p].used) p++;
+  if (p == KV_PEND) { kv_send_rep(s, me, m->src, m->term, KV_FAILED, 0, 0); return; }
+  uint64_t cmd = (1ull << 63) | ((uint64_t)(m->a & 3u) << 56) | ((uint64_t)((m->a >> 2) & 7u) << 53) |
+                 ((uint64_t)clerk << 48) | ((uint64_t)(m->b & 0xFFFFFFu) << 24) | (m->c & 0xFFFFFFu);
+  log_put(s, d, d->last + 1, d->term, cmd); /* start(), raft.rs:238-244 */
+  d->match[me] = d->last;
+  OPend* q = &s->pend[me][p];
+  q->used = 1; q->idx = d->last; q->clerk = clerk; q->seq = m->b; q->tag = m->term;
+}
+
 static void deliver(OSim* s, OMsg* m) {
   uint32_t me = m->dst;
+  if (me >= CLERK_HOST) { clerk_deliver(s, m); return; }
   ONode* d = &s->nd[me];
-  if (!d->alive || !d->conn || !s->nd[m->src].conn) {
+  if (!d->alive || !d->conn || !host_conn(s, m->src)) {
     s->r.drop_deliver++;
     rec_node(s, 0, 16, me, m->seq);
     return;
@@ -340,6 +458,11 @@ static void deliver(OSim* s, OMsg* m) {
   if (is_reply && m->inc != (uint8_t)d->inc) {
     s->r.drop_stale++;
     rec_node(s, 0, 17, me, m->seq);
+    return;
+  }
+  if (m->type == M_KV_REQ) {
+    kv_request(s, me, m);
+    rec_node(s, 0, m->type, me, m->seq);
     return;
   }
   if (m->term > d->term) { /* step down */
@@ -418,6 +541,7 @@ static void deliver(OSim* s, OMsg* m) {
       if (d->role == R_L && m->term == d->term && m->b > 0) on_ack(s, me, m->src, m->b);
       break;
   }
+  if (s->kv_mode) kv_flush(s, me);
   rec_node(s, 0, m->type, me, m->seq);
 }
 
@@ -441,9 +565,22 @@ static void on_timer(OSim* s, uint32_t me) {
   rec_node(s, 1, 0, me, 0);
 }
 
-/* drain the executor up to (target, TESTER): every message/timer with time <= target */
-static void run_until(OSim* s, uint32_t target) {
-  while (s->heap_n && (uint32_t)(s->heap[0].key >> 32) <= target) {
+static void client_step(OSim* s, uint32_t slot);
+
+/* a thread becomes runnable at (t, 2, tid) (SEMANTICS §8); slot 0 is the test body */
+static void thr_wake(OSim* s, uint32_t slot, uint32_t t) {
+  if (slot == 0) { s->mwake = t; return; }
+  OThr* th = &s->th[slot];
+  th->gen++;
+  heap_push(s, ((uint64_t)t << 32) | (2ull << 30) | th->tid, slot, th->gen);
+}
+
+/* drain the executor until the test body's wake-up key (mwake, 2, 0): every
+ * message / timer / other thread ordered before it (SEMANTICS §3, §8) */
+static void main_wait(OSim* s) {
+  for (;;) {
+    uint64_t mk = s->mwake == INF_T ? ~0ull : (((uint64_t)s->mwake << 32) | (2ull << 30));
+    if (!s->heap_n || s->heap[0].key >= mk) break;
     HEnt e = heap_pop(s);
     uint32_t cls = (uint32_t)(e.key >> 30) & 3u;
     if (cls == 1) {
@@ -453,6 +590,13 @@ static void run_until(OSim* s, uint32_t target) {
       count_event(s);
       s->r.ev_timer++;
       on_timer(s, e.ref);
+    } else if (cls == 2) {
+      OThr* th = &s->th[e.ref];
+      if (!th->live || e.gen != th->gen) continue; /* superseded wake-up */
+      s->now = (uint32_t)(e.key >> 32);
+      count_event(s);
+      s->r.ev_tester++;
+      client_step(s, e.ref);
     } else {
       OMsg m = s->pool[e.ref];
       s->free_stack[s->n_free++] = e.ref;
@@ -463,19 +607,26 @@ static void run_until(OSim* s, uint32_t target) {
       deliver(s, &m);
     }
   }
-  s->now = target;
+  if (s->mwake == INF_T) t_fail(s, MR_FAIL_SIM_BAD_PROGRAM); /* deadlock: nothing wakes main */
+  s->now = s->mwake;
 }
 
 /* ------------------------------------------------------------------ */
 /* tester API (src/raft/tester.rs)                                      */
 /* ------------------------------------------------------------------ */
-static void t_sleep(OSim* s, uint32_t us) { /* time::sleep */
+/* the test body blocks (its segment ends) until mwake; then one tester event */
+static void main_block(OSim* s) {
   rec_simple(s, 2, 0); /* the tester segment that ends here */
-  uint64_t target = (uint64_t)s->now + us;
-  if (target >= INF_T) t_fail(s, MR_FAIL_SIM_CAPACITY);
-  run_until(s, (uint32_t)target);
+  main_wait(s);
   count_event(s);
   s->r.ev_tester++;
+}
+
+static void t_sleep(OSim* s, uint32_t us) { /* time::sleep */
+  uint64_t target = (uint64_t)s->now + us;
+  if (target >= INF_T) { rec_simple(s, 2, 0); t_fail(s, MR_FAIL_SIM_CAPACITY); }
+  s->mwake = (uint32_t)target;
+  main_block(s);
 }
 
 static void t_draw(OSim* s, uint32_t w[4]) {
@@ -1021,6 +1172,126 @@ static void scn_snap_common(OSim* s, int disconnect, int reliable, int crash) { 
   t_end(s);
 }
 
+/* ------------------------------------------------------------------ */
+/* kvraft: clerks, client threads, generic_test (SEMANTICS §8-9)        */
+/* ------------------------------------------------------------------ */
+static void clerk_send(OSim* s, uint32_t slot) { /* one call_timeout attempt, client.rs:52-57 */
+  OClerk* c = &s->ck[slot];
+  c->tag++;
+  OMsg m;
+  m.type = M_KV_REQ; m.inc = 0; m.term = c->tag; m.a = c->op | (c->key << 2); m.b = c->seq;
+  m.c = c->elem; m.k = 0; m.v = 0;
+  net_send(s, CLERK_HOST + c->id, c->lh, &m);
+  c->waiting = 1; c->got = 0;
+  thr_wake(s, slot, s->now + 500000u); /* Duration::from_millis(500) */
+}
+
+static void clerk_begin(OSim* s, uint32_t slot, uint32_t op, uint32_t key, uint32_t elem) {
+  OClerk* c = &s->ck[slot];
+  c->seq++; c->op = op; c->key = key; c->elem = elem;
+  clerk_send(s, slot);
+}
+
+/* the clerk's thread woke (reply or timeout): 1 = call done (value in rval) */
+static int clerk_resume(OSim* s, uint32_t slot) {
+  OClerk* c = &s->ck[slot];
+  c->waiting = 0;
+  if (c->got) {
+    if (c->rstat == KV_OK) return 1;
+    c->lh = c->rstat == KV_WRONG_LEADER ? c->rhint : (c->lh + 1) % s->n;
+  } else {
+    c->lh = (c->lh + 1) % s->n;
+  }
+  clerk_send(s, slot);
+  return 0;
+}
+
+static int thr_bool(OSim* s, OThr* t, uint32_t p_q32) { /* rng.gen_bool on the thread's stream */
+  uint32_t ctr[4] = {t->tctr++, t->tid, ST_TESTER, 0}, w[4];
+  mro_philox4x32_10(ctr, s->key, w);
+  return w[0] < p_q32;
+}
+
+/* client task of generic_test, kvraft/tests.rs:109-131 */
+static void client_step(OSim* s, uint32_t slot) {
+  OThr* t = &s->th[slot];
+  OClerk* c = &s->ck[slot];
+  for (;;) {
+    switch (t->pc) {
+      case 0: clerk_begin(s, slot, KV_PUT, t->cli, 0); t->pc = 1; goto block; /* ck.put(&key, "") */
+      case 1: if (!clerk_resume(s, slot)) goto block; t->pc = 2; break;
+      case 2:
+        if (s->kv_done) goto finish;
+        if (thr_bool(s, t, 0x80000000u)) { clerk_begin(s, slot, KV_APPEND, t->cli, t->j); t->pc = 3; }
+        else { clerk_begin(s, slot, KV_GET, t->cli, 0); t->pc = 4; }
+        goto block;
+      case 3: if (!clerk_resume(s, slot)) goto block; t->j++; t->pc = 2; break;
+      case 4:
+        if (!clerk_resume(s, slot)) goto block;
+        if (!((c->rval >> 31) && (c->rval & 0x7FFFFFFFu) == t->j))
+          t_fail(s, MR_FAIL_KV_GET_WRONG); /* kvraft/tests.rs:127 */
+        t->pc = 2;
+        break;
+      default: t_fail(s, MR_FAIL_SIM_BAD_PROGRAM);
+    }
+  }
+block:
+  rec_simple(s, 2, t->tid & 0xFFu);
+  return;
+finish:
+  rec_simple(s, 2, t->tid & 0xFFu);
+  t->live = 0;
+  if (s->main_join == slot) s->mwake = s->now;
+}
+
+static void kv_spawn(OSim* s, uint32_t slot, uint32_t tid, uint32_t cli) { /* task::spawn_local */
+  OThr* t = &s->th[slot];
+  uint32_t gen = t->gen;
+  memset(t, 0, sizeof *t);
+  t->tid = tid; t->live = 1; t->cli = cli; t->gen = gen;
+  memset(&s->ck[slot], 0, sizeof s->ck[slot]);
+  s->ck[slot].id = tid; /* make_client order: ck = 0, then one clerk per client task */
+  thr_wake(s, slot, s->now);
+}
+
+static void t_join(OSim* s, uint32_t slot) { /* JoinHandle.await */
+  if (!s->th[slot].live) return;
+  s->main_join = slot;
+  s->mwake = INF_T;
+  main_block(s);
+  s->main_join = ~0u;
+}
+
+static uint32_t main_call(OSim* s, uint32_t op, uint32_t key, uint32_t elem) { /* ck.get etc. */
+  clerk_begin(s, 0, op, key, elem);
+  for (;;) {
+    main_block(s);
+    if (clerk_resume(s, 0)) return s->ck[0].rval;
+  }
+}
+
+static void scn_kv_generic(OSim* s, uint32_t nclients, int unreliable) { /* kvraft/tests.rs:65-220 */
+  t_new(s, 0); /* Tester::new (kvraft/tester.rs:27-56): start_server for every server */
+  if (unreliable) t_set_unreliable(s, 1);
+  s->kv_mode = 1;
+  s->th[0].live = 1;
+  memset(&s->ck[0], 0, sizeof s->ck[0]); /* ck = make_client(&t.all()): clerk 0 */
+  for (uint32_t i = 0; i < 3; i++) {
+    s->kv_done = 0;
+    for (uint32_t cli = 0; cli < nclients; cli++) kv_spawn(s, 1 + cli, 1 + nclients * i + cli, cli);
+    t_sleep(s, 5000000u);
+    s->kv_done = 1;
+    for (uint32_t cli = 0; cli < nclients; cli++) {
+      t_join(s, 1 + cli);
+      uint32_t j = s->th[1 + cli].j;
+      uint32_t v = main_call(s, KV_GET, cli, 0);
+      if (!(v >> 31)) t_fail(s, MR_FAIL_KV_APPEND_BAD);         /* kvraft/tests.rs:31-39 */
+      if ((v & 0x7FFFFFFFu) < j) t_fail(s, MR_FAIL_KV_MISSING); /* kvraft/tests.rs:25-30 */
+    }
+  }
+  t_end(s);
+}
+
 static int run_scenario(OSim* s) {
   switch (s->scenario) {
     case MR_SCN_INITIAL_ELECTION_2A: scn_initial_election(s); break;
@@ -1044,6 +1315,9 @@ static int run_scenario(OSim* s) {
     case MR_SCN_SNAPSHOT_INSTALL_UNRELIABLE_2D: scn_snap_common(s, 1, 0, 0); break;
     case MR_SCN_SNAPSHOT_INSTALL_CRASH_2D: scn_snap_common(s, 0, 1, 1); break;
     case MR_SCN_SNAPSHOT_INSTALL_UNRELIABLE_CRASH_2D: scn_snap_common(s, 0, 0, 1); break;
+    case MR_SCN_KV_BASIC_3A: scn_kv_generic(s, 1, 0); break;
+    case MR_SCN_KV_CONCURRENT_3A: scn_kv_generic(s, 5, 0); break;
+    case MR_SCN_KV_UNRELIABLE_3A: scn_kv_generic(s, 5, 1); break;
     default: return -1;
   }
   return 0;
@@ -1091,6 +1365,10 @@ static void sim_reset(OSim* s, uint64_t cluster) {
   s->n_free = s->cfg.msg_slots;
   for (uint32_t i = 0; i < s->n_free; i++) s->free_stack[i] = s->n_free - 1 - i;
   s->inflight = 0; s->heap_n = 0; s->t_ctr = 0;
+  s->kv_mode = 0; s->kv_done = 0; s->mwake = 0; s->main_join = ~0u;
+  memset(s->kv_n, 0, sizeof s->kv_n); memset(s->kv_ok, 0, sizeof s->kv_ok);
+  memset(s->kv_dedup, 0, sizeof s->kv_dedup); memset(s->pend, 0, sizeof s->pend);
+  memset(s->ck, 0, sizeof s->ck); memset(s->th, 0, sizeof s->th);
   memset(s->mask, 0, s->cfg.apply_cap);
   for (uint32_t i = 0; i < MR_MAX_NODES; i++) s->slen[i] = 1;
   memset(&s->r, 0, sizeof s->r);
@@ -1160,7 +1438,8 @@ static const char* k_names[MR_SCN_COUNT_] = {
     "unreliable_agree_2c", "figure_8_unreliable_2c", "reliable_churn_2c",
     "unreliable_churn_2c", "snapshot_basic_2d", "snapshot_install_2d",
     "snapshot_install_unreliable_2d", "snapshot_install_crash_2d",
-    "snapshot_install_unreliable_crash_2d", "figure_8_unreliable_crash"};
+    "snapshot_install_unreliable_crash_2d", "figure_8_unreliable_crash", "basic_3a",
+    "concurrent_3a", "unreliable_3a"};
 
 uint32_t mro_scenario_from_name(const char* name) {
   for (uint32_t i = 1; i < MR_SCN_COUNT_; i++)
@@ -1170,7 +1449,7 @@ uint32_t mro_scenario_from_name(const char* name) {
 
 int mro_cfg_init(mr_cfg* c, uint32_t scn) {
   static const uint8_t k_n[MR_SCN_COUNT_] = {0, 3, 3, 7, 5, 3, 5, 3, 3, 5, 3, 3, 5, 3,
-                                             5, 5, 5, 5, 5, 3, 3, 3, 3, 3, 5};
+                                             5, 5, 5, 5, 5, 3, 3, 3, 3, 3, 5, 5, 5, 5};
   if (scn == 0 || scn >= MR_SCN_COUNT_) return -1;
   memset(c, 0, sizeof *c);
   c->abi_version = MR_ABI_VERSION;
@@ -1182,9 +1461,11 @@ int mro_cfg_init(mr_cfg* c, uint32_t scn) {
   int fig8 = scn == MR_SCN_FIGURE_8_2C || scn == MR_SCN_FIGURE_8_UNRELIABLE_2C ||
              scn == MR_SCN_FIGURE_8_UNRELIABLE_CRASH;
   int snap = scn >= MR_SCN_SNAPSHOT_BASIC_2D && scn <= MR_SCN_SNAPSHOT_INSTALL_UNRELIABLE_CRASH_2D;
-  c->log_cap = fig8 ? 2048 : 256;
-  c->apply_cap = fig8 ? 2048 : (snap ? 1024 : 512);
-  c->msg_slots = 32;
+  int kv = scn >= MR_SCN_KV_BASIC_3A && scn <= MR_SCN_KV_UNRELIABLE_3A;
+  uint32_t kvcap = scn == MR_SCN_KV_CONCURRENT_3A ? 8192 : 2048;
+  c->log_cap = fig8 ? 2048 : (kv ? kvcap : 256);
+  c->apply_cap = fig8 ? 2048 : (snap ? 1024 : (kv ? kvcap : 512));
+  c->msg_slots = kv ? 64 : 32;
   c->ae_max = 16;
   c->hb_us = 50000;
   c->elect_lo_us = 150000;
@@ -1208,6 +1489,9 @@ const char* mro_fail_message(uint32_t code) {
     case MR_FAIL_APPLY_OUT_OF_ORDER: return "server apply out of order";
     case MR_FAIL_UNWRAP_NONE: return "called `Option::unwrap()` on a `None` value";
     case MR_FAIL_LOG_SIZE: return "log size too large";
+    case MR_FAIL_KV_GET_WRONG: return "get wrong value";
+    case MR_FAIL_KV_MISSING: return "missing element in Append result";
+    case MR_FAIL_KV_APPEND_BAD: return "duplicate or wrong order element in Append result";
     case MR_FAIL_SIM_CAPACITY: return "simulator capacity exceeded";
     case MR_FAIL_SIM_EVENT_LIMIT: return "simulator event limit exceeded";
     default: return "scenario assertion failed";

@@ -16,7 +16,7 @@ from madraft_amd import _abi
 
 pytestmark = pytest.mark.gpu
 
-SUPPORTED = [n for n in _abi.SCENARIOS if n and n not in _abi.UNSUPPORTED]
+SUPPORTED = [n for n in _abi.SCENARIOS if n and n not in _abi.GPU_UNSUPPORTED]
 COUNTER_KEYS = ["events", "ev_msg", "ev_timer", "ev_tester", "msgs_sent", "drop_clog",
                 "drop_loss", "drop_overflow", "drop_deliver", "drop_stale", "elections",
                 "leaders_elected", "applies", "snapshots", "installs", "entries_shipped",
