@@ -32,9 +32,9 @@ SCENARIOS = [
 SCENARIO_ID = {n: i for i, n in enumerate(SCENARIOS) if n}
 # tests that still need multi-threaded tester programs (spawn_local); not built yet
 UNSUPPORTED = {"unreliable_agree_2c", "reliable_churn_2c", "unreliable_churn_2c"}
-# kvraft generic_test (src/kvraft/tests.rs); oracle-only until the HIP path lands
+# kvraft generic_test (src/kvraft/tests.rs:65-238), BASELINE config 5
 KV_TESTS = ["basic_3a", "concurrent_3a", "unreliable_3a"]
-GPU_UNSUPPORTED = UNSUPPORTED | set(KV_TESTS)
+GPU_UNSUPPORTED = set(UNSUPPORTED)
 
 FAIL_NAMES = {
     0: "PASS", 1: "ONE_LEADER_NONE", 2: "MULTI_LEADER_TERM", 3: "TERM_DISAGREE",

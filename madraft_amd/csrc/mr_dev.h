@@ -24,7 +24,7 @@ namespace mr {
 // ---- node flag word (one u32 per node): role[0:2) voted[4:8) (15 = none)
 //      inc[8:16) votes[16:24); started / connected are cluster bit masks (CS_ALIVE, CS_CONN)
 enum : uint32_t { R_F = 0, R_C = 1, R_L = 2, R_DOWN = 3 };
-enum : uint32_t { M_RV_REQ = 1, M_RV_REP, M_AE_REQ, M_AE_REP, M_IS_REQ, M_IS_REP };
+enum : uint32_t { M_RV_REQ = 1, M_RV_REP, M_AE_REQ, M_AE_REP, M_IS_REQ, M_IS_REP, M_KV_REQ, M_KV_REP };
 enum : uint32_t { ST_TESTER = 1, ST_ELECT = 2, ST_NET = 3 };
 
 // per-cluster u32 counters (part of cs32); the last three are maxima
@@ -44,7 +44,8 @@ constexpr uint32_t T_NV = 16;  // u64 script arrays (count_2b / concurrent_start
 enum : uint32_t {
   CS_CODE, CS_VTIME, CS_NOW, CS_EVENTS, CS_MSGS, CS_INFLIGHT, CS_NETMODE, CS_TCTR, CS_TRACEN,
   CS_MSLOT, CS_CONN, CS_ALIVE, CS_TPC, CS_TWAKE, CS_TRES, CS_TL, CS_TH = CS_TL + T_NL, CS_CNT = CS_TH + T_NH,
-  CS__N = CS_CNT + CNT__N
+  CS_KVDONE = CS_CNT + CNT__N, CS_MJOIN, CS_CWAKE, CS_CTID, CS_CSLOT,  // kvraft (SEMANTICS §8-9)
+  CS__N
 };
 // cs64 [C64__N][C]: per-cluster u64 scalars
 enum : uint32_t { C64_FREE, C64_DIGEST, C64_MMIN, C64_THV, C64_TV, C64__N = C64_TV + T_NV };
@@ -69,6 +70,22 @@ struct alignas(16) LE {
   uint64_t val;
 };
 
+// ---- kvraft (SEMANTICS §8-9); arrays allocated for the kvraft scenarios only
+enum : uint32_t { KV_GET = 0, KV_PUT = 1, KV_APPEND = 2 };
+enum : uint32_t { KV_OK = 0, KV_WRONG_LEADER = 1, KV_FAILED = 2 };
+constexpr uint32_t CLERK_HOST = 8;  // clerk c is host 8 + c
+constexpr uint32_t KV_SLOTS = 6;    // tester thread / clerk slots: 0 = test body + ck, 1 + cli
+constexpr uint32_t KV_PEND = 8;     // pending requests per server
+// kt32 [KT__N][KV_SLOTS][C]: thread + clerk per slot
+enum : uint32_t {
+  KT_TID, KT_LIVE, KT_PC, KT_J, KT_CLI, KT_TCTR, KT_WAKE, KT_ID, KT_LH, KT_SEQ, KT_TAG, KT_NCTR,
+  KT_WAITING, KT_GOT, KT_RSTAT, KT_RHINT, KT_RVAL, KT_OP, KT_KEY, KT_ELEM, KT__N
+};
+// kv32 [C][n][KVREC]: per-server KV state: n[key] at 0..7, ok mask at 8, dedup[clerk] at
+// 16..31, pending request p at 32 + 4p: {index (0 = free), clerk | seq24 << 5 |
+// ready << 29 | status << 30, tag, value}
+constexpr uint32_t KVR_N = 0, KVR_OK = 8, KVR_DEDUP = 16, KVR_PEND = 32, KVREC = 64;
+
 // one tester apply-checker index (StorageHandle, tester.rs:366-428): the value
 // the first applier stored and the mask of servers whose log holds it
 struct alignas(16) SE {
@@ -90,11 +107,15 @@ struct Dev {
   LE* log;  // [C][n][log_cap] ring per node
   LE* pay;  // [C][M][K] AppendEntries payload per message slot
   SE* stor;         // [C][apply_cap]   tester storage (tester.rs:366-428)
+  uint32_t* kt32;   // [KT__N][KV_SLOTS][C] (kvraft only)
+  uint32_t* kv32;   // [C][n][KVREC]        (kvraft only)
   mr_event* trace;  // [trace_clusters][trace_cap]
   uint32_t* remaining;  // clusters without verdict after a step launch
   unsigned long long* prof;  // [PROF_SLOTS] wave-cycle profile (MR_PROF builds only)
 };
 constexpr uint32_t PROF_SLOTS = 64;
+
+constexpr bool is_kv(uint32_t s) { return s >= MR_SCN_KV_BASIC_3A && s <= MR_SCN_KV_UNRELIABLE_3A; }
 
 // one step-kernel instance per scenario (mr_kernel.hip launch_step_t<S>)
 template <uint32_t S>
@@ -102,6 +123,7 @@ hipError_t launch_step_t(const Dev& D, uint32_t budget, hipStream_t s);
 #define MR_ALL_SCNS                                                                       \
   MR_INST(1) MR_INST(2) MR_INST(3) MR_INST(4) MR_INST(5) MR_INST(6) MR_INST(7) MR_INST(8) \
   MR_INST(9) MR_INST(10) MR_INST(11) MR_INST(12) MR_INST(13) MR_INST(14) MR_INST(16)      \
-  MR_INST(19) MR_INST(20) MR_INST(21) MR_INST(22) MR_INST(23) MR_INST(24)
+  MR_INST(19) MR_INST(20) MR_INST(21) MR_INST(22) MR_INST(23) MR_INST(24) MR_INST(25)     \
+  MR_INST(26) MR_INST(27)
 
 }  // namespace mr

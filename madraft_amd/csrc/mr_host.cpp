@@ -177,7 +177,7 @@ int mr_batch_create(const mr_cfg* cfg, mr_batch** out) {
   if (validate(cfg) != 0) return -1;
   const uint32_t scn = cfg->scenario;
   if (scn == MR_SCN_UNRELIABLE_AGREE_2C || scn == MR_SCN_RELIABLE_CHURN_2C ||
-      scn == MR_SCN_UNRELIABLE_CHURN_2C || scn >= MR_SCN_KV_BASIC_3A)
+      scn == MR_SCN_UNRELIABLE_CHURN_2C)
     return set_err(std::string("scenario needs concurrent tester tasks (not built yet): ") +
                    k_names[scn]);
 
@@ -220,6 +220,10 @@ int mr_batch_create(const mr_cfg* cfg, mr_batch** out) {
   add(&D.log, C * n * cfg->log_cap);
   add(&D.pay, C * M * K);
   add(&D.stor, C * cfg->apply_cap);
+  if (is_kv(scn)) {  // kvraft thread / clerk table and per-server KV records
+    add(&D.kt32, (size_t)KT__N * KV_SLOTS * C);
+    add(&D.kv32, (size_t)KVREC * n * C);
+  }
   add(&D.trace, (size_t)D.trace_clusters * D.trace_cap);
   add(&D.remaining, 1);
   add(&D.prof, PROF_SLOTS);
@@ -242,7 +246,7 @@ int mr_batch_create(const mr_cfg* cfg, mr_batch** out) {
   b->bytes = total;
   char* p = static_cast<char*>(b->base);
   for (auto& it : items) {
-    *it.p = p;
+    *it.p = it.bytes ? p : nullptr;
     p += (it.bytes + 255) & ~size_t(255);
   }
   if (hipMemset(b->D.prof, 0, PROF_SLOTS * sizeof(unsigned long long)) != hipSuccess) {
@@ -266,6 +270,8 @@ int mr_batch_reset(mr_batch* b, uint64_t seed_base) {
   b->D.seed0 = seed_base + b->cfg.cluster_base;
   HIPCHK(hipSetDevice(b->cfg.device));
   HIPCHK(hipMemsetAsync(b->D.stor, 0, (size_t)b->D.C * b->D.apply_cap * sizeof(SE), b->stream));
+  if (b->D.kv32)
+    HIPCHK(hipMemsetAsync(b->D.kv32, 0, (size_t)b->D.C * b->D.n * KVREC * sizeof(uint32_t), b->stream));
   HIPCHK(launch_reset(b->D, b->stream));
   HIPCHK(hipStreamSynchronize(b->stream));
   return 0;

@@ -38,6 +38,7 @@ constexpr uint32_t ELECTION_US = 1000000;  // RAFT_ELECTION_TIMEOUT, tests.rs:18
 struct X {
   uint32_t c, now, events, msgs_sent, inflight, code, trace_n, mslot, netmode, t_ctr;
   uint32_t sleep_us, yield, twake;  // twake: the tester's next wake-up (CS_TWAKE)
+  uint32_t cwake, ctid, cslot;      // kvraft: earliest client thread (wake, tid, slot)
   uint32_t conn, alive;  // node bit masks: connected (net clog state), started (tester.rs:24-25)
   uint64_t free_mask, digest, mmin;
   uint32_t timer[MR_MAX_NODES];  // node timers (election / heartbeat deadline), INF_T = none
@@ -258,11 +259,11 @@ DI void rescan_min(const Dev& D, X& x) {
 
 // madsim net send from node `src` (whose state is `s`) (tester.rs:127-137,
 // :147-149). Returns the slot or -1 if the message is dropped.
-DI int net_send(const Dev& D, X& x, uint32_t src, NC& s, uint32_t dst, uint32_t type,
+DI int net_send(const Dev& D, X& x, uint32_t src, uint32_t& nctr, uint32_t dst, uint32_t type,
                 uint32_t inc, uint32_t term, uint32_t a, uint32_t b, uint32_t c, uint64_t v,
                 uint32_t k) {
   uint32_t seq = x.msgs_sent++;
-  uint32_t ctr = s.nctr++;
+  uint32_t ctr = nctr++;
   if (!bit(x.conn, src) || !bit(x.conn, dst)) { CADD(CNT_DROP_CLOG, 1u); return -1; }
   uint32_t w0, w1;
   philox(D, x, ctr, src, ST_NET, w0, w1);
@@ -372,11 +373,14 @@ DI uint32_t n_committed(const Dev& D, X& x, uint32_t idx, uint64_t& v) {  // tes
 // changes and its applies, in ascending peer order.
 enum : uint32_t { SEND_NONE = 0, SEND_REPLY, SEND_APPEND, SEND_VOTE };
 
+#include "mr_kv.inc"
+
 // the tester's applier (tester.rs:302-325) with push_and_check
 // (tester.rs:366-396) inlined: committed entries are walked in batches of AC
 // whose loads (log entry, storage mask / value) are all issued before any is
 // used — entries have distinct indices, so a batch never reads what it writes.
-DI void node_apply(const Dev& D, X& x, uint32_t me, NC& d) {
+template <bool KV>
+DI void node_apply(const Dev& D, X& x, uint32_t me, NC& d, bool& kvready) {
   const bool snapmode = (x.netmode >> 1) & 1u;
   SE* const sb = D.stor + (size_t)x.c * D.apply_cap;
   uint32_t len = d.slen;
@@ -415,6 +419,7 @@ DI void node_apply(const Dev& D, X& x, uint32_t me, NC& d) {
         NSV(me) = e[j].val;
         CADD(CNT_SNAPSHOTS, 1u);
       }
+      if constexpr (KV) kv_apply(D, x, me, i, e[j].val, kvready);
     }
     PROF(P_AP_CHECK);
   }
@@ -468,9 +473,11 @@ DI void ae_load_batch(const Dev& D, const X& x, uint32_t me, const NC& d, uint32
   }
 }
 
+template <bool KV>
 DI void node_event(const Dev& D, X& x, bool is_msg, uint32_t tnode, uint32_t slot,
                    uint32_t seq) {
   uint32_t me = tnode, src = 0, type = 0, inc = 0, k = 0, mterm = 0, ma = 0, mb = 0, mc = 0;
+  bool kvready = false;
   uint32_t hdr_bits = 0;
   if (is_msg) {
     const uint4 m0 = reinterpret_cast<const uint4*>(MSP(slot))[0];
@@ -484,6 +491,12 @@ DI void node_event(const Dev& D, X& x, bool is_msg, uint32_t tnode, uint32_t slo
     x.inflight--;
     rescan_min(D, x);
     PROF(P_DECODE);
+    if constexpr (KV) {
+      if (me >= CLERK_HOST) {  // KV_REP at a clerk host
+        clerk_deliver(D, x, me, src, mterm, ma, mb, mc, seq);
+        return;
+      }
+    }
   }
   NC d = load_node(D, x, me);
   PROF(P_LOAD);
@@ -503,6 +516,15 @@ DI void node_event(const Dev& D, X& x, bool is_msg, uint32_t tnode, uint32_t slo
       rec_node(D, x, 0, 17, me, seq, d);
       PROF(P_DROP);
       return;
+    }
+    if constexpr (KV) {
+      if (type == M_KV_REQ) {  // no Raft term: handled before the step-down rule
+        kv_request(D, x, me, d, src, mterm, ma, mb, mc);
+        if (x.code != RUN) return;
+        store_node(D, x, me, d);
+        rec_node(D, x, 0, type, me, seq, d);
+        return;
+      }
     }
     if (mterm > d.term) {  // step down
       uint32_t was = f_role(d.f);
@@ -643,7 +665,7 @@ DI void node_event(const Dev& D, X& x, bool is_msg, uint32_t tnode, uint32_t slo
     PROF(P_ELECT);
   }
   if (d.applied < d.commit) {  // committed entries reach the tester's applier
-    node_apply(D, x, me, d);
+    node_apply<KV>(D, x, me, d, kvready);
     if (x.code != RUN) return;
     PROF(P_APPLY);
   }
@@ -691,7 +713,7 @@ DI void node_event(const Dev& D, X& x, bool is_msg, uint32_t tnode, uint32_t slo
       }
     }
     PROF(P_S_SETUP);
-    int s = net_send(D, x, me, d, p, st, sinc, d.term, sa, sb, sc, sv, sk);
+    int s = net_send(D, x, me, d.nctr, p, st, sinc, d.term, sa, sb, sc, sv, sk);
     if (x.code != RUN) return;
     PROF(P_S_NET);
     if (s >= 0 && sk) {  // zero-copy payload: entries prev+1 .. prev+sk stay in this log
@@ -701,6 +723,12 @@ DI void node_event(const Dev& D, X& x, bool is_msg, uint32_t tnode, uint32_t slo
     }
   }
   if (plo_acc <= phi_acc) pend_note(D, x, me, d, plo_acc, phi_acc);
+  if constexpr (KV) {
+    if (kvready) {
+      kv_flush(D, x, me, d);
+      if (x.code != RUN) return;
+    }
+  }
   PROF(P_SEND);
   store_node(D, x, me, d);
   rec_node(D, x, is_msg ? 0u : 1u, kind, me, is_msg ? seq : 0u, d);
@@ -833,9 +861,14 @@ DI void tester(const Dev& D, X& x) {
   for (int guard = 0;; guard++) {
     if (guard > 4096) { fail(D, x, MR_FAIL_SIM_BAD_PROGRAM); return; }
     if (t.helper != H_NONE) {  // a multi-event tester call in progress
-      bool done = t.helper == H_ONE   ? one_step(D, x, t)
-                  : t.helper == H_COL ? col_step(D, x, t)
-                                      : wait_step(D, x, t);
+      bool done;
+      if constexpr (is_kv(S)) {
+        done = t.helper == H_CALL ? call_step(D, x, t) : join_step(D, x, t);
+      } else {
+        done = t.helper == H_ONE   ? one_step(D, x, t)
+               : t.helper == H_COL ? col_step(D, x, t)
+                                   : wait_step(D, x, t);
+      }
       if (x.code != RUN) return;
       if (!done) break;  // it slept
       t.helper = H_NONE;
@@ -845,10 +878,12 @@ DI void tester(const Dev& D, X& x) {
     if (x.yield) break;
     if (t.helper == H_NONE) { fail(D, x, MR_FAIL_SIM_BAD_PROGRAM); return; }
   }
-  rec_simple(D, x, 2, 0);  // time::sleep closes this tester segment (SEMANTICS §7)
-  uint64_t target = (uint64_t)x.now + x.sleep_us;
-  if (target >= INF_T) { fail(D, x, MR_FAIL_SIM_CAPACITY); return; }
-  x.twake = (uint32_t)target;
+  rec_simple(D, x, 2, 0);  // the test body blocks: this tester segment ends (SEMANTICS §7)
+  if (x.yield != 2) {  // time::sleep; 2 = clerk call / join (x.twake already set)
+    uint64_t target = (uint64_t)x.now + x.sleep_us;
+    if (target >= INF_T) { fail(D, x, MR_FAIL_SIM_CAPACITY); return; }
+    x.twake = (uint32_t)target;
+  }
   CS(CS_TPC) = t.pc | (t.helper << 24);
   CS(CS_TRES) = t.res;
 #pragma unroll
@@ -881,6 +916,7 @@ __global__ void __launch_bounds__(STEP_BLOCK, MR_WAVES_PER_EU) step_kernel(Dev D
     x.inflight = CS(CS_INFLIGHT); x.trace_n = CS(CS_TRACEN); x.mslot = CS(CS_MSLOT);
     x.netmode = CS(CS_NETMODE); x.t_ctr = CS(CS_TCTR);
     x.conn = CS(CS_CONN); x.alive = CS(CS_ALIVE); x.twake = CS(CS_TWAKE);
+    if constexpr (is_kv(S)) { x.cwake = CS(CS_CWAKE); x.ctid = CS(CS_CTID); x.cslot = CS(CS_CSLOT); }
 #pragma unroll
     for (uint32_t d = 0; d < MR_MAX_NODES; d++) x.timer[d] = d < D.n ? ND(NF_TIMER, d) : INF_T;
     x.free_mask = C64(C64_FREE); x.digest = C64(C64_DIGEST); x.mmin = C64(C64_MMIN);
@@ -894,7 +930,7 @@ __global__ void __launch_bounds__(STEP_BLOCK, MR_WAVES_PER_EU) step_kernel(Dev D
   PROF(P_PRO);
   uint64_t key = 0;
   uint32_t cls = CLS_NONE, node = 0;
-  bool need = true;
+  bool need = true, tcli = false;
   for (uint32_t it = 0; it < budget; it++) {
     asm volatile("" : "+v"(x.c));  // no LICM of per-lane addresses: recompute, do not keep live
     PROF(P_TAIL);
@@ -903,6 +939,11 @@ __global__ void __launch_bounds__(STEP_BLOCK, MR_WAVES_PER_EU) step_kernel(Dev D
     if (run && need) {  // next event: min over tester wake-up, node timers, earliest message
       key = ((uint64_t)x.twake << 32) | (2ull << 30);
       cls = CLS_TESTER;
+      if constexpr (is_kv(S)) {  // the earliest client thread (tie = tid)
+        const uint64_t kc = ((uint64_t)x.cwake << 32) | (2ull << 30) | x.ctid;
+        tcli = kc < key;
+        if (tcli) key = kc;
+      }
 #pragma unroll
       for (uint32_t d = 0; d < MR_MAX_NODES; d++) {  // timers of absent nodes are INF_T
         uint64_t kt = ((uint64_t)x.timer[d] << 32) | (1ull << 30) | d;
@@ -927,16 +968,25 @@ __global__ void __launch_bounds__(STEP_BLOCK, MR_WAVES_PER_EU) step_kernel(Dev D
     const bool mine = MR_MERGE_NODE ? (tpick ? cls == CLS_TESTER : cls != CLS_TESTER) : cls == pick;
     PROF(P_SEL);
     if (!run || !mine) continue;
+    if (is_kv(S) && (uint32_t)(key >> 32) == INF_T) {  // nothing can wake the test body
+      fail(D, x, MR_FAIL_SIM_BAD_PROGRAM);
+      continue;
+    }
     x.now = (uint32_t)(key >> 32);
     need = true;
     x.events++;
     if (x.events > D.max_events) { fail(D, x, MR_FAIL_SIM_EVENT_LIMIT); continue; }
     if (cls != CLS_TESTER) {
       CADD(cls == CLS_MSG ? CNT_EV_MSG : CNT_EV_TIMER, 1u);
-      node_event(D, x, cls == CLS_MSG, node, x.mslot, ((uint32_t)key & 0x3FFFFFFFu) >> 5);
+      node_event<is_kv(S)>(D, x, cls == CLS_MSG, node, x.mslot, ((uint32_t)key & 0x3FFFFFFFu) >> 5);
     } else {
       CADD(CNT_EV_TESTER, 1u);
-      tester<S>(D, x);
+      if constexpr (is_kv(S)) {
+        if (tcli) kv_client_step(D, x, x.cslot);
+        else tester<S>(D, x);
+      } else {
+        tester<S>(D, x);
+      }
       PROF(P_TESTER);
     }
   }
@@ -955,6 +1005,7 @@ __global__ void __launch_bounds__(STEP_BLOCK, MR_WAVES_PER_EU) step_kernel(Dev D
   CS(CS_INFLIGHT) = x.inflight; CS(CS_TRACEN) = x.trace_n; CS(CS_MSLOT) = x.mslot;
   CS(CS_NETMODE) = x.netmode; CS(CS_TCTR) = x.t_ctr;
   CS(CS_CONN) = x.conn; CS(CS_ALIVE) = x.alive; CS(CS_TWAKE) = x.twake;
+  if constexpr (is_kv(S)) { CS(CS_CWAKE) = x.cwake; CS(CS_CTID) = x.ctid; CS(CS_CSLOT) = x.cslot; }
 #pragma unroll
   for (uint32_t d = 0; d < MR_MAX_NODES; d++)
     if (d < D.n) ND(NF_TIMER, d) = x.timer[d];
@@ -992,6 +1043,15 @@ __global__ void __launch_bounds__(256) reset_kernel(Dev D) {
     for (uint32_t p = 0; p < D.n; p++) { PR(PF_NEXT, d, p) = 0; PR(PF_MATCH, d, p) = 0; }
   }
   for (uint32_t s = 0; s < D.M; s++) MKEY(s) = ~0ull;
+  CS(CS_MJOIN) = 0xFFFFFFFFu;
+  CS(CS_CWAKE) = INF_T;
+  if (D.kt32) {  // kvraft: slot 0 = the test body + ck (clerk 0); client slots empty
+    for (uint32_t s = 0; s < KV_SLOTS; s++) {
+      for (uint32_t f = 0; f < KT__N; f++) KT(f, s) = 0u;
+      KT(KT_WAKE, s) = INF_T;
+    }
+    KT(KT_LIVE, 0) = 1u;
+  }
 }
 
 // counters_reduce: per-GPU sums / maxima / verdict histogram / first failing

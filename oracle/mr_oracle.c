@@ -442,7 +442,7 @@ static void kv_request(OSim* s, uint32_t me, OMsg* m) {
   log_put(s, d, d->last + 1, d->term, cmd); /* start(), raft.rs:238-244 */
   d->match[me] = d->last;
   OPend* q = &s->pend[me][p];
-  q->used = 1; q->idx = d->last; q->clerk = clerk; q->seq = m->b; q->tag = m->term;
+  q->used = 1; q->idx = d->last; q->clerk = clerk; q->seq = m->b & 0xFFFFFFu; q->tag = m->term;
 }
 
 static void deliver(OSim* s, OMsg* m) {

@@ -79,6 +79,14 @@ def test_snapshot_7_nodes(hip, oracle):
     assert cnt["installs"] > 0 and cnt["snapshots"] > 0
 
 
+def test_kv_unreliable_traced(hip, oracle):
+    """BASELINE config 5 shape: 5 servers + 5 clerk threads over the unreliable
+    net; traced clusters compared record by record (clerk deliveries, client
+    thread segments, server KV events)."""
+    code, cnt = compare(hip, oracle, "unreliable_3a", 128, traced=8)
+    assert cnt["drop_loss"] > 0 and cnt["applies"] > 0
+
+
 def test_sharded_cluster_base(hip, oracle):
     """A shard (cluster_base != 0) computes the same seeds as the oracle's global ids."""
     compare(hip, oracle, "figure_8_unreliable_2c", 128, traced=2, first=5000)
@@ -107,6 +115,7 @@ def test_step_budget_independence(hip):
     ("fail_agree_2b", 65536, dict(nodes=5, unreliable=True)),     # BASELINE config 2
     ("figure_8_unreliable_2c", 131072, {}),                        # config 3, one GPU's shard
     ("snapshot_install_unreliable_2d", 65536, dict(nodes=7)),      # config 4 shape
+    ("unreliable_3a", 65536, {}),                                  # config 5: kvraft clerks
 ])
 def test_baseline_sizes(hip, oracle, test, clusters, kw):
     with hip.Batch(test, clusters, **kw) as b:
