@@ -31,10 +31,10 @@ SCENARIOS = [
 ]
 SCENARIO_ID = {n: i for i, n in enumerate(SCENARIOS) if n}
 # tests that still need multi-threaded tester programs (spawn_local); not built yet
-UNSUPPORTED = {"unreliable_agree_2c", "reliable_churn_2c", "unreliable_churn_2c"}
+UNSUPPORTED = set()
 # kvraft generic_test (src/kvraft/tests.rs:65-238), BASELINE config 5
 KV_TESTS = ["basic_3a", "concurrent_3a", "unreliable_3a"]
-GPU_UNSUPPORTED = set(UNSUPPORTED)
+GPU_UNSUPPORTED = set()
 
 FAIL_NAMES = {
     0: "PASS", 1: "ONE_LEADER_NONE", 2: "MULTI_LEADER_TERM", 3: "TERM_DISAGREE",

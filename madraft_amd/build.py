@@ -24,7 +24,7 @@ def _stale(out, srcs):
 
 # step-kernel instances (one per scenario id, mr_dev.h MR_ALL_SCNS) are split
 # over several translation units of mr_kernel.hip compiled in parallel
-SCN_IDS = [1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 16, 19, 20, 21, 22, 23, 24, 25, 26, 27]
+SCN_IDS = list(range(1, 28))
 N_GROUPS = 8
 
 

@@ -44,7 +44,8 @@ constexpr uint32_t T_NV = 16;  // u64 script arrays (count_2b / concurrent_start
 enum : uint32_t {
   CS_CODE, CS_VTIME, CS_NOW, CS_EVENTS, CS_MSGS, CS_INFLIGHT, CS_NETMODE, CS_TCTR, CS_TRACEN,
   CS_MSLOT, CS_CONN, CS_ALIVE, CS_TPC, CS_TWAKE, CS_TRES, CS_TL, CS_TH = CS_TL + T_NL, CS_CNT = CS_TH + T_NH,
-  CS_KVDONE = CS_CNT + CNT__N, CS_MJOIN, CS_CWAKE, CS_CTID, CS_CSLOT,  // kvraft (SEMANTICS §8-9)
+  CS_KVDONE = CS_CNT + CNT__N, CS_MJOIN, CS_CWAKE, CS_CTID, CS_CSLOT,  // tester threads (SEMANTICS §8-9)
+  CS_NLIVE,  // live spawned threads
   CS__N
 };
 // cs64 [C64__N][C]: per-cluster u64 scalars
@@ -76,11 +77,16 @@ enum : uint32_t { KV_OK = 0, KV_WRONG_LEADER = 1, KV_FAILED = 2 };
 constexpr uint32_t CLERK_HOST = 8;  // clerk c is host 8 + c
 constexpr uint32_t KV_SLOTS = 6;    // tester thread / clerk slots: 0 = test body + ck, 1 + cli
 constexpr uint32_t KV_PEND = 8;     // pending requests per server
-// kt32 [KT__N][KV_SLOTS][C]: thread + clerk per slot
+// kt32 [KT__N][nthr(S)][C]: a spawned tester thread (+ its clerk, kvraft) per slot.
+// Words KT_W.. are the thread's own frame: kvraft clerk fields, churn client
+// (x lo/hi, index, timeout step, values), or a one() task (helper frame h[0..4], cmd).
 enum : uint32_t {
   KT_TID, KT_LIVE, KT_PC, KT_J, KT_CLI, KT_TCTR, KT_WAKE, KT_ID, KT_LH, KT_SEQ, KT_TAG, KT_NCTR,
   KT_WAITING, KT_GOT, KT_RSTAT, KT_RHINT, KT_RVAL, KT_OP, KT_KEY, KT_ELEM, KT__N
 };
+constexpr uint32_t KT_W = KT_ID;
+constexpr uint32_t JOIN_ALL = 0xFFFFFFFEu;
+constexpr uint32_t CHURN_VCAP = 512;  // values one churn client may record (tests.rs:763-797)
 // kv32 [C][n][KVREC]: per-server KV state: n[key] at 0..7, ok mask at 8, dedup[clerk] at
 // 16..31, pending request p at 32 + 4p: {index (0 = free), clerk | seq24 << 5 |
 // ready << 29 | status << 30, tag, value}
@@ -109,6 +115,9 @@ struct Dev {
   SE* stor;         // [C][apply_cap]   tester storage (tester.rs:366-428)
   uint32_t* kt32;   // [KT__N][KV_SLOTS][C] (kvraft only)
   uint32_t* kv32;   // [C][n][KVREC]        (kvraft only)
+  uint64_t* cval;   // [C][3][CHURN_VCAP]   churn clients' committed values (churn only)
+  uint32_t* cidx;   // [C][3][CHURN_VCAP]   ... and the index each was seen at
+  uint32_t nthr;    // thread slots of kt32 (0 = none)
   mr_event* trace;  // [trace_clusters][trace_cap]
   uint32_t* remaining;  // clusters without verdict after a step launch
   unsigned long long* prof;  // [PROF_SLOTS] wave-cycle profile (MR_PROF builds only)
@@ -116,6 +125,14 @@ struct Dev {
 constexpr uint32_t PROF_SLOTS = 64;
 
 constexpr bool is_kv(uint32_t s) { return s >= MR_SCN_KV_BASIC_3A && s <= MR_SCN_KV_UNRELIABLE_3A; }
+constexpr bool is_churn(uint32_t s) {
+  return s == MR_SCN_RELIABLE_CHURN_2C || s == MR_SCN_UNRELIABLE_CHURN_2C;
+}
+// tester thread slots (slot 0 = the test body): kvraft 1 + 5 clients, churn 1 + 3
+// clients, unreliable_agree_2c up to 63 concurrent one() tasks
+constexpr uint32_t nthr(uint32_t s) {
+  return is_kv(s) ? KV_SLOTS : is_churn(s) ? 4u : s == MR_SCN_UNRELIABLE_AGREE_2C ? 64u : 0u;
+}
 
 // one step-kernel instance per scenario (mr_kernel.hip launch_step_t<S>)
 template <uint32_t S>
@@ -124,6 +141,6 @@ hipError_t launch_step_t(const Dev& D, uint32_t budget, hipStream_t s);
   MR_INST(1) MR_INST(2) MR_INST(3) MR_INST(4) MR_INST(5) MR_INST(6) MR_INST(7) MR_INST(8) \
   MR_INST(9) MR_INST(10) MR_INST(11) MR_INST(12) MR_INST(13) MR_INST(14) MR_INST(16)      \
   MR_INST(19) MR_INST(20) MR_INST(21) MR_INST(22) MR_INST(23) MR_INST(24) MR_INST(25)     \
-  MR_INST(26) MR_INST(27)
+  MR_INST(26) MR_INST(27) MR_INST(15) MR_INST(17) MR_INST(18)
 
 }  // namespace mr

@@ -141,9 +141,11 @@ int mr_cfg_init(mr_cfg* c, uint32_t scn) {
              scn == MR_SCN_FIGURE_8_UNRELIABLE_CRASH;
   int snap = scn >= MR_SCN_SNAPSHOT_BASIC_2D && scn <= MR_SCN_SNAPSHOT_INSTALL_UNRELIABLE_CRASH_2D;
   int kv = scn >= MR_SCN_KV_BASIC_3A && scn <= MR_SCN_KV_UNRELIABLE_3A;
-  uint32_t kvcap = scn == MR_SCN_KV_CONCURRENT_3A ? 8192 : 2048;
-  c->log_cap = fig8 ? 2048 : (kv ? kvcap : 256);
-  c->apply_cap = fig8 ? 2048 : (snap ? 1024 : (kv ? kvcap : 512));
+  int churn = scn == MR_SCN_RELIABLE_CHURN_2C || scn == MR_SCN_UNRELIABLE_CHURN_2C;
+  uint32_t cap = fig8 ? 2048 : kv ? (scn == MR_SCN_KV_CONCURRENT_3A ? 8192 : 2048)
+               : churn ? 4096 : scn == MR_SCN_UNRELIABLE_AGREE_2C ? 1024 : 0;
+  c->log_cap = cap ? cap : 256;
+  c->apply_cap = cap ? cap : (snap ? 1024 : 512);
   c->msg_slots = kv ? 64 : 32;
   c->ae_max = 16;
   c->hb_us = 50000;
@@ -176,10 +178,6 @@ int mr_batch_create(const mr_cfg* cfg, mr_batch** out) {
   *out = nullptr;
   if (validate(cfg) != 0) return -1;
   const uint32_t scn = cfg->scenario;
-  if (scn == MR_SCN_UNRELIABLE_AGREE_2C || scn == MR_SCN_RELIABLE_CHURN_2C ||
-      scn == MR_SCN_UNRELIABLE_CHURN_2C)
-    return set_err(std::string("scenario needs concurrent tester tasks (not built yet): ") +
-                   k_names[scn]);
 
   mr_batch* b = new mr_batch();
   b->cfg = *cfg;
@@ -220,9 +218,15 @@ int mr_batch_create(const mr_cfg* cfg, mr_batch** out) {
   add(&D.log, C * n * cfg->log_cap);
   add(&D.pay, C * M * K);
   add(&D.stor, C * cfg->apply_cap);
-  if (is_kv(scn)) {  // kvraft thread / clerk table and per-server KV records
-    add(&D.kt32, (size_t)KT__N * KV_SLOTS * C);
-    add(&D.kv32, (size_t)KVREC * n * C);
+  // scenario-only arrays: spawned tester threads, kvraft servers, churn values
+  static const uint8_t k_thr[MR_SCN_COUNT_] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 64,
+                                               0, 4, 4, 0, 0, 0, 0, 0, 0, 6, 6, 6};
+  D.nthr = k_thr[scn];
+  if (D.nthr) add(&D.kt32, (size_t)KT__N * D.nthr * C);
+  if (is_kv(scn)) add(&D.kv32, (size_t)KVREC * n * C);
+  if (is_churn(scn)) {
+    add(&D.cval, (size_t)3 * CHURN_VCAP * C);
+    add(&D.cidx, (size_t)3 * CHURN_VCAP * C);
   }
   add(&D.trace, (size_t)D.trace_clusters * D.trace_cap);
   add(&D.remaining, 1);

@@ -864,6 +864,10 @@ DI void tester(const Dev& D, X& x) {
       bool done;
       if constexpr (is_kv(S)) {
         done = t.helper == H_CALL ? call_step(D, x, t) : join_step(D, x, t);
+      } else if constexpr (nthr(S) > 0) {
+        done = t.helper == H_ONE    ? one_step(D, x, t)
+               : t.helper == H_WAIT ? wait_step(D, x, t)
+                                    : join_step(D, x, t);  // H_JOIN: join_all
       } else {
         done = t.helper == H_ONE   ? one_step(D, x, t)
                : t.helper == H_COL ? col_step(D, x, t)
@@ -916,7 +920,7 @@ __global__ void __launch_bounds__(STEP_BLOCK, MR_WAVES_PER_EU) step_kernel(Dev D
     x.inflight = CS(CS_INFLIGHT); x.trace_n = CS(CS_TRACEN); x.mslot = CS(CS_MSLOT);
     x.netmode = CS(CS_NETMODE); x.t_ctr = CS(CS_TCTR);
     x.conn = CS(CS_CONN); x.alive = CS(CS_ALIVE); x.twake = CS(CS_TWAKE);
-    if constexpr (is_kv(S)) { x.cwake = CS(CS_CWAKE); x.ctid = CS(CS_CTID); x.cslot = CS(CS_CSLOT); }
+    if constexpr (nthr(S) > 0) { x.cwake = CS(CS_CWAKE); x.ctid = CS(CS_CTID); x.cslot = CS(CS_CSLOT); }
 #pragma unroll
     for (uint32_t d = 0; d < MR_MAX_NODES; d++) x.timer[d] = d < D.n ? ND(NF_TIMER, d) : INF_T;
     x.free_mask = C64(C64_FREE); x.digest = C64(C64_DIGEST); x.mmin = C64(C64_MMIN);
@@ -939,7 +943,7 @@ __global__ void __launch_bounds__(STEP_BLOCK, MR_WAVES_PER_EU) step_kernel(Dev D
     if (run && need) {  // next event: min over tester wake-up, node timers, earliest message
       key = ((uint64_t)x.twake << 32) | (2ull << 30);
       cls = CLS_TESTER;
-      if constexpr (is_kv(S)) {  // the earliest client thread (tie = tid)
+      if constexpr (nthr(S) > 0) {  // the earliest spawned thread (tie = tid)
         const uint64_t kc = ((uint64_t)x.cwake << 32) | (2ull << 30) | x.ctid;
         tcli = kc < key;
         if (tcli) key = kc;
@@ -968,7 +972,7 @@ __global__ void __launch_bounds__(STEP_BLOCK, MR_WAVES_PER_EU) step_kernel(Dev D
     const bool mine = MR_MERGE_NODE ? (tpick ? cls == CLS_TESTER : cls != CLS_TESTER) : cls == pick;
     PROF(P_SEL);
     if (!run || !mine) continue;
-    if (is_kv(S) && (uint32_t)(key >> 32) == INF_T) {  // nothing can wake the test body
+    if (nthr(S) > 0 && (uint32_t)(key >> 32) == INF_T) {  // nothing can wake the test body
       fail(D, x, MR_FAIL_SIM_BAD_PROGRAM);
       continue;
     }
@@ -981,8 +985,8 @@ __global__ void __launch_bounds__(STEP_BLOCK, MR_WAVES_PER_EU) step_kernel(Dev D
       node_event<is_kv(S)>(D, x, cls == CLS_MSG, node, x.mslot, ((uint32_t)key & 0x3FFFFFFFu) >> 5);
     } else {
       CADD(CNT_EV_TESTER, 1u);
-      if constexpr (is_kv(S)) {
-        if (tcli) kv_client_step(D, x, x.cslot);
+      if constexpr (nthr(S) > 0) {
+        if (tcli) thr_step<S>(D, x, x.cslot);
         else tester<S>(D, x);
       } else {
         tester<S>(D, x);
@@ -1005,7 +1009,7 @@ __global__ void __launch_bounds__(STEP_BLOCK, MR_WAVES_PER_EU) step_kernel(Dev D
   CS(CS_INFLIGHT) = x.inflight; CS(CS_TRACEN) = x.trace_n; CS(CS_MSLOT) = x.mslot;
   CS(CS_NETMODE) = x.netmode; CS(CS_TCTR) = x.t_ctr;
   CS(CS_CONN) = x.conn; CS(CS_ALIVE) = x.alive; CS(CS_TWAKE) = x.twake;
-  if constexpr (is_kv(S)) { CS(CS_CWAKE) = x.cwake; CS(CS_CTID) = x.ctid; CS(CS_CSLOT) = x.cslot; }
+  if constexpr (nthr(S) > 0) { CS(CS_CWAKE) = x.cwake; CS(CS_CTID) = x.ctid; CS(CS_CSLOT) = x.cslot; }
 #pragma unroll
   for (uint32_t d = 0; d < MR_MAX_NODES; d++)
     if (d < D.n) ND(NF_TIMER, d) = x.timer[d];
@@ -1045,8 +1049,8 @@ __global__ void __launch_bounds__(256) reset_kernel(Dev D) {
   for (uint32_t s = 0; s < D.M; s++) MKEY(s) = ~0ull;
   CS(CS_MJOIN) = 0xFFFFFFFFu;
   CS(CS_CWAKE) = INF_T;
-  if (D.kt32) {  // kvraft: slot 0 = the test body + ck (clerk 0); client slots empty
-    for (uint32_t s = 0; s < KV_SLOTS; s++) {
+  if (D.kt32) {  // spawned threads: slot 0 = the test body (+ ck, clerk 0); others empty
+    for (uint32_t s = 0; s < D.nthr; s++) {
       for (uint32_t f = 0; f < KT__N; f++) KT(f, s) = 0u;
       KT(KT_WAKE, s) = INF_T;
     }

@@ -46,6 +46,9 @@ enum { KV_OK = 0, KV_WRONG_LEADER = 1, KV_FAILED = 2 };
 #define MAX_CLERKS 16u
 #define KV_SLOTS 6u     /* thread / clerk slots: 0 = main + ck, 1 + cli = client cli */
 #define KV_PEND 8u
+#define MAX_THR 64u     /* tester thread slots (unreliable_agree_2c: concurrent one() tasks) */
+#define JOIN_ALL 0xFFFFFFFEu
+#define CHURN_VCAP 512u /* values a churn client may record (tests.rs:763-797) */
 #define INF_T 0xFFFFFFFFu
 #define LOSS_Q32 429496729u /* floor(0.1 * 2^32), tester.rs:130 */
 
@@ -82,7 +85,11 @@ typedef struct {
   uint32_t op, key, elem;
 } OClerk;
 typedef struct {
-  uint32_t tid, live, pc, j, cli, tctr, gen, done_at;
+  uint32_t tid, live, pc, j, cli, tctr, gen;
+  /* churn client (tests.rs:763-797) */
+  uint64_t xv; uint32_t idx, has, toi, nval;
+  /* one() task (tester.rs:216-262) */
+  uint64_t cmd; uint32_t t0, starts, index, t1, ph, expected, retry;
 } OThr;
 typedef struct { uint32_t used, idx, clerk, seq, tag, ready, status, value; } OPend;
 
@@ -102,7 +109,9 @@ typedef struct {
   uint32_t kv_mode, kv_done, next_tid, mwake, main_join;
   uint32_t kv_n[MR_MAX_NODES][8], kv_ok[MR_MAX_NODES], kv_dedup[MR_MAX_NODES][MAX_CLERKS];
   OPend pend[MR_MAX_NODES][KV_PEND];
-  OClerk ck[KV_SLOTS]; OThr th[KV_SLOTS];
+  OClerk ck[KV_SLOTS]; OThr th[MAX_THR];
+  uint64_t* cval; uint32_t* cidx; /* churn values [3][CHURN_VCAP] + their indices */
+  uint32_t churn_stop;
   /* results */
   mro_result r;
   mr_event* trace; size_t trace_cap, n_trace;
@@ -1212,8 +1221,19 @@ static int thr_bool(OSim* s, OThr* t, uint32_t p_q32) { /* rng.gen_bool on the t
   return w[0] < p_q32;
 }
 
+/* a tester thread finished (its segment record is written): wake a joining test body */
+static void thr_finish(OSim* s, uint32_t slot) {
+  s->th[slot].live = 0;
+  if (s->main_join == slot) s->mwake = s->now;
+  if (s->main_join == JOIN_ALL) {
+    uint32_t live = 0;
+    for (uint32_t k = 1; k < MAX_THR; k++) live += s->th[k].live;
+    if (!live) s->mwake = s->now;
+  }
+}
+
 /* client task of generic_test, kvraft/tests.rs:109-131 */
-static void client_step(OSim* s, uint32_t slot) {
+static void kv_client_step(OSim* s, uint32_t slot) {
   OThr* t = &s->th[slot];
   OClerk* c = &s->ck[slot];
   for (;;) {
@@ -1240,8 +1260,185 @@ block:
   return;
 finish:
   rec_simple(s, 2, t->tid & 0xFFu);
-  t->live = 0;
-  if (s->main_join == slot) s->mwake = s->now;
+  thr_finish(s, slot);
+}
+
+/* ---- raft tests with spawn_local (tests.rs:662-686, 743-856) ---- */
+static uint64_t thr_entry(OSim* s, OThr* t) { /* random.gen_entry() on the thread's stream */
+  uint32_t ctr[4] = {t->tctr++, t->tid, ST_TESTER, 0}, w[4];
+  mro_philox4x32_10(ctr, s->key, w);
+  return ((uint64_t)w[1] << 32) | w[0];
+}
+
+/* cfn, the churn client (tests.rs:763-797); slot 1 + me */
+static void churn_step(OSim* s, uint32_t slot) {
+  static const uint32_t TO_MS[5] = {10, 20, 50, 100, 200};
+  OThr* t = &s->th[slot];
+  uint32_t me = slot - 1, idx, term;
+  for (int guard = 0;; guard++) {
+    if (guard > 4096) t_fail(s, MR_FAIL_SIM_BAD_PROGRAM); /* a segment must end (SEMANTICS §8) */
+    if (t->pc == 0) {
+      if (s->churn_stop) { rec_simple(s, 2, t->tid & 0xFFu); thr_finish(s, slot); return; }
+      t->xv = thr_entry(s, t);
+      t->has = 0;
+      for (uint32_t i = 0; i < s->n; i++) { /* try them all, maybe one of them is a leader */
+        if (!t_is_started(s, i)) continue;
+        if (t_start(s, i, t->xv, &idx, &term)) { t->idx = idx; t->has = 1; }
+      }
+      if (!t->has) { s->th[slot].j = 79 + me * 17; goto sleep_ms; }
+      t->toi = 0;
+      t->pc = 1;
+    }
+    /* pc 1: for to in [10, 20, 50, 100, 200] { n_committed(index) ...; sleep(to) } */
+    uint32_t cnt; uint64_t v;
+    n_committed(s, t->idx, &cnt, &v);
+    if (cnt > 0) {
+      if (v == t->xv) {
+        if (t->nval >= CHURN_VCAP) t_fail(s, MR_FAIL_SIM_CAPACITY);
+        s->cval[me * CHURN_VCAP + t->nval] = v;
+        s->cidx[me * CHURN_VCAP + t->nval] = t->idx;
+        t->nval++;
+      }
+      t->pc = 0;
+      continue;
+    }
+    s->th[slot].j = TO_MS[t->toi++];
+    if (t->toi == 5) t->pc = 0;
+    goto sleep_ms;
+  }
+sleep_ms:
+  rec_simple(s, 2, t->tid & 0xFFu);
+  thr_wake(s, slot, s->now + s->th[slot].j * 1000u);
+}
+
+/* one(cmd, expected, retry) as a spawned task (tester.rs:216-262), unreliable_agree_2c */
+static void one_thr_step(OSim* s, uint32_t slot) {
+  OThr* t = &s->th[slot];
+  uint32_t term;
+  for (;;) {
+    if (t->ph == 1) {
+      if (!(s->now - t->t0 < 10000000u)) t_fail(s, MR_FAIL_ONE_NO_AGREEMENT);
+      int have = 0;
+      for (uint32_t k = 0; k < s->n; k++) {
+        t->starts = (t->starts + 1) % s->n;
+        if (!t_is_connected(s, t->starts) || !t_is_started(s, t->starts)) continue;
+        if (t_start(s, t->starts, t->cmd, &t->index, &term)) { have = 1; break; }
+      }
+      if (!have) { rec_simple(s, 2, t->tid & 0xFFu); thr_wake(s, slot, s->now + 50000u); return; }
+      t->t1 = s->now;
+      t->ph = 2;
+    }
+    if (s->now - t->t1 < 2000000u) {
+      uint32_t cnt; uint64_t v;
+      n_committed(s, t->index, &cnt, &v);
+      if (cnt > 0 && cnt >= t->expected && v == t->cmd) {
+        rec_simple(s, 2, t->tid & 0xFFu);
+        thr_finish(s, slot);
+        return;
+      }
+      rec_simple(s, 2, t->tid & 0xFFu);
+      thr_wake(s, slot, s->now + 20000u);
+      return;
+    }
+    if (!t->retry) t_fail(s, MR_FAIL_ONE_NO_AGREEMENT);
+    t->ph = 1;
+  }
+}
+
+static void client_step(OSim* s, uint32_t slot) {
+  switch (s->scenario) {
+    case MR_SCN_RELIABLE_CHURN_2C:
+    case MR_SCN_UNRELIABLE_CHURN_2C: churn_step(s, slot); break;
+    case MR_SCN_UNRELIABLE_AGREE_2C: one_thr_step(s, slot); break;
+    default: kv_client_step(s, slot); break;
+  }
+}
+
+static void t_join_all(OSim* s) { /* future::join_all(handles).await: wakes when the last ends */
+  uint32_t live = 0;
+  for (uint32_t k = 1; k < MAX_THR; k++) live += s->th[k].live;
+  if (!live) return;
+  s->main_join = JOIN_ALL;
+  s->mwake = INF_T;
+  main_block(s);
+  s->main_join = ~0u;
+}
+
+static void thr_spawn(OSim* s, uint32_t slot, uint32_t tid) { /* task::spawn_local */
+  OThr* t = &s->th[slot];
+  uint32_t gen = t->gen;
+  memset(t, 0, sizeof *t);
+  t->tid = tid; t->live = 1; t->gen = gen;
+  thr_wake(s, slot, s->now);
+}
+
+static void scn_churn(OSim* s, int unreliable) { /* internal_churn, tests.rs:755-856 */
+  uint32_t n = s->n;
+  t_new(s, 0);
+  t_set_unreliable(s, unreliable);
+  s->churn_stop = 0;
+  s->th[0].live = 1;
+  for (uint32_t i = 0; i < 3; i++) thr_spawn(s, 1 + i, 1 + i); /* ncli = 3 */
+  for (int it = 0; it < 20; it++) {
+    if (t_bool(s, 858993459u)) { uint32_t i = t_range(s, 0, n); t_disconnect(s, i); } /* 0.2 */
+    if (t_bool(s, 0x80000000u)) {
+      uint32_t i = t_range(s, 0, n);
+      if (!t_is_started(s, i)) t_start1(s, i);
+      t_connect(s, i);
+    }
+    if (t_bool(s, 858993459u)) {
+      uint32_t i = t_range(s, 0, n);
+      if (t_is_started(s, i)) t_crash1(s, i);
+    }
+    t_sleep(s, ELECTION_US * 7 / 10);
+  }
+  t_sleep(s, ELECTION_US);
+  t_set_unreliable(s, 0);
+  for (uint32_t i = 0; i < n; i++) {
+    if (!t_is_started(s, i)) t_start1(s, i);
+    t_connect(s, i);
+  }
+  s->churn_stop = 1;
+  t_sleep(s, ELECTION_US);
+  uint32_t last = t_one(s, t_entry(s), n, 1);
+  uint64_t v;
+  for (uint32_t index = 1; index <= last; index++) t_wait(s, index, n, 0, 0, &v);
+  t_join_all(s);
+  for (uint32_t c = 0; c < 3; c++)
+    for (uint32_t k = 0; k < s->th[1 + c].nval; k++) {
+      uint64_t v1 = s->cval[c * CHURN_VCAP + k];
+      int found = 0;
+      for (uint32_t index = 1; index <= last && !found; index++) {
+        uint32_t cnt; uint64_t w;
+        n_committed(s, index, &cnt, &w);
+        found = cnt > 0 && w == v1;
+      }
+      if (!found) t_fail(s, MR_FAIL_CHURN_VALUE); /* tests.rs:852 */
+    }
+  t_end(s);
+}
+
+static void scn_unreliable_agree(OSim* s) { /* tests.rs:662-686 */
+  uint32_t n = s->n, tid = 1;
+  t_new(s, 0);
+  t_set_unreliable(s, 1);
+  s->th[0].live = 1;
+  for (uint32_t iters = 1; iters < 50; iters++) {
+    for (uint32_t j = 0; j < 4; j++) {
+      uint32_t slot = 1;
+      while (slot < MAX_THR && s->th[slot].live) slot++;
+      if (slot == MAX_THR) t_fail(s, MR_FAIL_SIM_CAPACITY);
+      thr_spawn(s, slot, tid++);
+      OThr* t = &s->th[slot];
+      t->cmd = 100 * iters + j; t->expected = 1; t->retry = 1;
+      t->t0 = s->now; t->starts = 0; t->ph = 1;
+    }
+    t_one(s, iters, 1, 1);
+  }
+  t_set_unreliable(s, 0);
+  t_join_all(s);
+  t_one(s, 100, n, 1);
+  t_end(s);
 }
 
 static void kv_spawn(OSim* s, uint32_t slot, uint32_t tid, uint32_t cli) { /* task::spawn_local */
@@ -1315,6 +1512,9 @@ static int run_scenario(OSim* s) {
     case MR_SCN_SNAPSHOT_INSTALL_UNRELIABLE_2D: scn_snap_common(s, 1, 0, 0); break;
     case MR_SCN_SNAPSHOT_INSTALL_CRASH_2D: scn_snap_common(s, 0, 1, 1); break;
     case MR_SCN_SNAPSHOT_INSTALL_UNRELIABLE_CRASH_2D: scn_snap_common(s, 0, 0, 1); break;
+    case MR_SCN_UNRELIABLE_AGREE_2C: scn_unreliable_agree(s); break;
+    case MR_SCN_RELIABLE_CHURN_2C: scn_churn(s, 0); break;
+    case MR_SCN_UNRELIABLE_CHURN_2C: scn_churn(s, 1); break;
     case MR_SCN_KV_BASIC_3A: scn_kv_generic(s, 1, 0); break;
     case MR_SCN_KV_CONCURRENT_3A: scn_kv_generic(s, 5, 0); break;
     case MR_SCN_KV_UNRELIABLE_3A: scn_kv_generic(s, 5, 1); break;
@@ -1338,6 +1538,8 @@ static int sim_alloc(OSim* s, const mr_cfg* cfg) {
     s->nd[i].lterm = (uint32_t*)malloc(cfg->log_cap * sizeof(uint32_t));
     s->nd[i].lval = (uint64_t*)malloc(cfg->log_cap * sizeof(uint64_t));
   }
+  s->cval = (uint64_t*)malloc(3 * CHURN_VCAP * sizeof(uint64_t));
+  s->cidx = (uint32_t*)malloc(3 * CHURN_VCAP * sizeof(uint32_t));
   s->mask = (uint8_t*)malloc(cfg->apply_cap);
   s->sval = (uint64_t*)malloc(cfg->apply_cap * sizeof(uint64_t));
   return 0;
@@ -1345,7 +1547,7 @@ static int sim_alloc(OSim* s, const mr_cfg* cfg) {
 
 static void sim_free(OSim* s) {
   for (uint32_t i = 0; i < MR_MAX_NODES; i++) { free(s->nd[i].lterm); free(s->nd[i].lval); }
-  free(s->mask); free(s->sval); free(s->heap);
+  free(s->mask); free(s->sval); free(s->heap); free(s->cval); free(s->cidx);
 }
 
 static void sim_reset(OSim* s, uint64_t cluster) {
@@ -1368,7 +1570,7 @@ static void sim_reset(OSim* s, uint64_t cluster) {
   s->kv_mode = 0; s->kv_done = 0; s->mwake = 0; s->main_join = ~0u;
   memset(s->kv_n, 0, sizeof s->kv_n); memset(s->kv_ok, 0, sizeof s->kv_ok);
   memset(s->kv_dedup, 0, sizeof s->kv_dedup); memset(s->pend, 0, sizeof s->pend);
-  memset(s->ck, 0, sizeof s->ck); memset(s->th, 0, sizeof s->th);
+  memset(s->ck, 0, sizeof s->ck); memset(s->th, 0, sizeof s->th); s->churn_stop = 0;
   memset(s->mask, 0, s->cfg.apply_cap);
   for (uint32_t i = 0; i < MR_MAX_NODES; i++) s->slen[i] = 1;
   memset(&s->r, 0, sizeof s->r);
@@ -1462,9 +1664,11 @@ int mro_cfg_init(mr_cfg* c, uint32_t scn) {
              scn == MR_SCN_FIGURE_8_UNRELIABLE_CRASH;
   int snap = scn >= MR_SCN_SNAPSHOT_BASIC_2D && scn <= MR_SCN_SNAPSHOT_INSTALL_UNRELIABLE_CRASH_2D;
   int kv = scn >= MR_SCN_KV_BASIC_3A && scn <= MR_SCN_KV_UNRELIABLE_3A;
-  uint32_t kvcap = scn == MR_SCN_KV_CONCURRENT_3A ? 8192 : 2048;
-  c->log_cap = fig8 ? 2048 : (kv ? kvcap : 256);
-  c->apply_cap = fig8 ? 2048 : (snap ? 1024 : (kv ? kvcap : 512));
+  int churn = scn == MR_SCN_RELIABLE_CHURN_2C || scn == MR_SCN_UNRELIABLE_CHURN_2C;
+  uint32_t cap = fig8 ? 2048 : kv ? (scn == MR_SCN_KV_CONCURRENT_3A ? 8192 : 2048)
+               : churn ? 4096 : scn == MR_SCN_UNRELIABLE_AGREE_2C ? 1024 : 0;
+  c->log_cap = cap ? cap : 256;
+  c->apply_cap = cap ? cap : (snap ? 1024 : 512);
   c->msg_slots = kv ? 64 : 32;
   c->ae_max = 16;
   c->hb_us = 50000;
