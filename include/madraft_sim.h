@@ -72,6 +72,9 @@ enum mr_scenario {
   MR_SCN_KV_BASIC_3A = 25,               /* kvraft/tests.rs:222-226: 1 client        */
   MR_SCN_KV_CONCURRENT_3A = 26,          /* kvraft/tests.rs:228-232: 5 clients       */
   MR_SCN_KV_UNRELIABLE_3A = 27,          /* kvraft/tests.rs:234-238: 5, unreliable   */
+  /* shard_ctrler (src/shard_ctrler/tests.rs) over 3 servers */
+  MR_SCN_CTRL_BASIC_4A = 28,             /* shard_ctrler/tests.rs:24-166  */
+  MR_SCN_CTRL_MULTI_4A = 29,             /* shard_ctrler/tests.rs:168-299 */
   MR_SCN_COUNT_
 };
 
@@ -112,6 +115,18 @@ enum mr_fail {
   MR_FAIL_KV_GET_WRONG = 27,      /* kvraft/tests.rs:127 "get wrong value, key {:?}" */
   MR_FAIL_KV_MISSING = 28,        /* kvraft/tests.rs:25-30 "missing element {:?} in Append result" */
   MR_FAIL_KV_APPEND_BAD = 29,     /* kvraft/tests.rs:31-39 duplicate / wrong order element */
+  MR_FAIL_CTRL_NGROUPS = 30,      /* shard_ctrler/tester.rs:117 assert_eq!(c.groups.len(), ..) */
+  MR_FAIL_CTRL_MISSING = 31,      /* shard_ctrler/tester.rs:120 "missing group {}" */
+  MR_FAIL_CTRL_INVALID = 32,      /* shard_ctrler/tester.rs:125-130 "shard {} -> invalid group {}" */
+  MR_FAIL_CTRL_IMBALANCED = 33,   /* shard_ctrler/tester.rs:142-148 "imbalanced sharding" */
+  MR_FAIL_CTRL_SERVERS = 34,      /* shard_ctrler/tests.rs:51,53,198-202,210 "wrong servers for gid" */
+  MR_FAIL_CTRL_HISTORY = 35,      /* shard_ctrler/tests.rs:70 historical query != config */
+  MR_FAIL_CTRL_MOVE_NUM = 36,     /* shard_ctrler/tests.rs:91 "Move should increase Tester.Num" */
+  MR_FAIL_CTRL_MOVE_WRONG = 37,   /* shard_ctrler/tests.rs:97 "shard {} wrong group" */
+  MR_FAIL_CTRL_MINIMAL_JOIN = 38, /* shard_ctrler/tests.rs:135,251 "non-minimal transfer after Join()s" */
+  MR_FAIL_CTRL_MINIMAL_LEAVE = 39,/* shard_ctrler/tests.rs:154,269 "non-minimal transfer after Leave()s" */
+  MR_FAIL_CTRL_NO_LEADER = 40,    /* shard_ctrler/tests.rs:282,289 "Leader not found" */
+  MR_FAIL_CTRL_SAME_CONFIG = 41,  /* shard_ctrler/tests.rs:294 assert_eq!(c, c1) */
   /* simulator limits (not reference panics): a cluster that hits one is reported, never passed */
   MR_FAIL_SIM_CAPACITY = 60,      /* a log / apply / sequence capacity of the config was exceeded */
   MR_FAIL_SIM_EVENT_LIMIT = 61,   /* cfg.max_events processed without a verdict */

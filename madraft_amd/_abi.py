@@ -27,7 +27,7 @@ SCENARIOS = [
     "unreliable_churn_2c", "snapshot_basic_2d", "snapshot_install_2d",
     "snapshot_install_unreliable_2d", "snapshot_install_crash_2d",
     "snapshot_install_unreliable_crash_2d", "figure_8_unreliable_crash", "basic_3a",
-    "concurrent_3a", "unreliable_3a",
+    "concurrent_3a", "unreliable_3a", "basic_4a", "multi_4a",
 ]
 SCENARIO_ID = {n: i for i, n in enumerate(SCENARIOS) if n}
 # tests that still need multi-threaded tester programs (spawn_local); not built yet
@@ -44,7 +44,10 @@ FAIL_NAMES = {
     16: "EXPECTED_INDEX2", 17: "NO_MAJORITY_COMMIT", 18: "UNEXPECTED_INDEX", 19: "CMD_MISSING",
     20: "TERM_CHANGED", 21: "RPC_INITIAL", 22: "START_FAILED", 23: "WRONG_VALUE",
     24: "RPC_TOO_MANY", 25: "RPC_IDLE", 26: "CHURN_VALUE", 27: "KV_GET_WRONG", 28: "KV_MISSING",
-    29: "KV_APPEND_BAD", 60: "SIM_CAPACITY",
+    29: "KV_APPEND_BAD", 30: "CTRL_NGROUPS", 31: "CTRL_MISSING", 32: "CTRL_INVALID",
+    33: "CTRL_IMBALANCED", 34: "CTRL_SERVERS", 35: "CTRL_HISTORY", 36: "CTRL_MOVE_NUM",
+    37: "CTRL_MOVE_WRONG", 38: "CTRL_MINIMAL_JOIN", 39: "CTRL_MINIMAL_LEAVE", 40: "CTRL_NO_LEADER",
+    41: "CTRL_SAME_CONFIG", 60: "SIM_CAPACITY",
     61: "SIM_EVENT_LIMIT", 62: "SIM_BAD_PROGRAM", 0xFFFF: "RUNNING",
 }
 

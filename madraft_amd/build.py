@@ -24,7 +24,7 @@ def _stale(out, srcs):
 
 # step-kernel instances (one per scenario id, mr_dev.h MR_ALL_SCNS) are split
 # over several translation units of mr_kernel.hip compiled in parallel
-SCN_IDS = list(range(1, 28))
+SCN_IDS = list(range(1, 30))
 N_GROUPS = 8
 
 

@@ -46,6 +46,7 @@ enum : uint32_t {
   CS_MSLOT, CS_CONN, CS_ALIVE, CS_TPC, CS_TWAKE, CS_TRES, CS_TL, CS_TH = CS_TL + T_NL, CS_CNT = CS_TH + T_NH,
   CS_KVDONE = CS_CNT + CNT__N, CS_MJOIN, CS_CWAKE, CS_CTID, CS_CSLOT,  // tester threads (SEMANTICS §8-9)
   CS_NLIVE,  // live spawned threads
+  CS_NOPS,   // shard_ctrler: clerk operations so far
   CS__N
 };
 // cs64 [C64__N][C]: per-cluster u64 scalars
@@ -90,7 +91,16 @@ constexpr uint32_t CHURN_VCAP = 512;  // values one churn client may record (tes
 // kv32 [C][n][KVREC]: per-server KV state: n[key] at 0..7, ok mask at 8, dedup[clerk] at
 // 16..31, pending request p at 32 + 4p: {index (0 = free), clerk | seq24 << 5 |
 // ready << 29 | status << 30, tag, value}
-constexpr uint32_t KVR_N = 0, KVR_OK = 8, KVR_DEDUP = 16, KVR_PEND = 32, KVREC = 64;
+constexpr uint32_t KVR_N = 0, KVR_OK = 8, KVR_NCFG = 9, KVR_DEDUP = 16, KVR_PEND = 32, KVREC = 64;
+// ---- shard_ctrler (SEMANTICS §10): per-server append-only config store and a
+// per-cluster table of clerk operations (the log command names an operation)
+constexpr uint32_t N_SHARDS = 10;  // shard_ctrler/mod.rs:9
+constexpr uint32_t CFG_CAP = 128, CFG_G = 32, OP_CAP = 256;
+// cfg32 [C][n][CFG_CAP][CFGW]: num, shards[10], ng, gid[32], addr[32]
+enum : uint32_t { CF_NUM = 0, CF_SHARDS = 1, CF_NG = 11, CF_GID = 12, CF_ADDR = 44, CFGW = 80 };
+// op32 [C][OP_CAP][OPW]: type, a (num / shard), b (gid), ng, gid[5], addr[5]
+enum : uint32_t { OP_TYPE = 0, OP_A, OP_B, OP_NG, OP_GID, OP_ADDR = 9, OPW = 16 };
+enum : uint32_t { CT_QUERY = 0, CT_JOIN = 1, CT_LEAVE = 2, CT_MOVE = 3 };
 
 // one tester apply-checker index (StorageHandle, tester.rs:366-428): the value
 // the first applier stored and the mask of servers whose log holds it
@@ -117,6 +127,8 @@ struct Dev {
   uint32_t* kv32;   // [C][n][KVREC]        (kvraft only)
   uint64_t* cval;   // [C][3][CHURN_VCAP]   churn clients' committed values (churn only)
   uint32_t* cidx;   // [C][3][CHURN_VCAP]   ... and the index each was seen at
+  uint32_t* cfg32;  // [C][n][CFG_CAP][CFGW] shard_ctrler config stores
+  uint32_t* op32;   // [C][OP_CAP][OPW]       shard_ctrler operations
   uint32_t nthr;    // thread slots of kt32 (0 = none)
   mr_event* trace;  // [trace_clusters][trace_cap]
   uint32_t* remaining;  // clusters without verdict after a step launch
@@ -125,13 +137,17 @@ struct Dev {
 constexpr uint32_t PROF_SLOTS = 64;
 
 constexpr bool is_kv(uint32_t s) { return s >= MR_SCN_KV_BASIC_3A && s <= MR_SCN_KV_UNRELIABLE_3A; }
+constexpr bool is_ctrl(uint32_t s) { return s == MR_SCN_CTRL_BASIC_4A || s == MR_SCN_CTRL_MULTI_4A; }
+// scenarios served by the clerk / server request path (kvraft + shard_ctrler)
+constexpr bool is_svc(uint32_t s) { return is_kv(s) || is_ctrl(s); }
 constexpr bool is_churn(uint32_t s) {
   return s == MR_SCN_RELIABLE_CHURN_2C || s == MR_SCN_UNRELIABLE_CHURN_2C;
 }
 // tester thread slots (slot 0 = the test body): kvraft 1 + 5 clients, churn 1 + 3
 // clients, unreliable_agree_2c up to 63 concurrent one() tasks
 constexpr uint32_t nthr(uint32_t s) {
-  return is_kv(s) ? KV_SLOTS : is_churn(s) ? 4u : s == MR_SCN_UNRELIABLE_AGREE_2C ? 64u : 0u;
+  return is_kv(s) ? KV_SLOTS : is_ctrl(s) ? 11u : is_churn(s) ? 4u
+         : s == MR_SCN_UNRELIABLE_AGREE_2C ? 64u : 0u;
 }
 
 // one step-kernel instance per scenario (mr_kernel.hip launch_step_t<S>)
@@ -141,6 +157,6 @@ hipError_t launch_step_t(const Dev& D, uint32_t budget, hipStream_t s);
   MR_INST(1) MR_INST(2) MR_INST(3) MR_INST(4) MR_INST(5) MR_INST(6) MR_INST(7) MR_INST(8) \
   MR_INST(9) MR_INST(10) MR_INST(11) MR_INST(12) MR_INST(13) MR_INST(14) MR_INST(16)      \
   MR_INST(19) MR_INST(20) MR_INST(21) MR_INST(22) MR_INST(23) MR_INST(24) MR_INST(25)     \
-  MR_INST(26) MR_INST(27) MR_INST(15) MR_INST(17) MR_INST(18)
+  MR_INST(26) MR_INST(27) MR_INST(15) MR_INST(17) MR_INST(18) MR_INST(28) MR_INST(29)
 
 }  // namespace mr

@@ -54,10 +54,10 @@ const char* k_names[MR_SCN_COUNT_] = {
     "unreliable_churn_2c", "snapshot_basic_2d", "snapshot_install_2d",
     "snapshot_install_unreliable_2d", "snapshot_install_crash_2d",
     "snapshot_install_unreliable_crash_2d", "figure_8_unreliable_crash", "basic_3a",
-    "concurrent_3a", "unreliable_3a"};
+    "concurrent_3a", "unreliable_3a", "basic_4a", "multi_4a"};
 // servers per test (tests.rs `let servers = ..`)
 const uint8_t k_nodes[MR_SCN_COUNT_] = {0, 3, 3, 7, 5, 3, 5, 3, 3, 5, 3, 3, 5, 3,
-                                        5, 5, 5, 5, 5, 3, 3, 3, 3, 3, 5, 5, 5, 5};
+                                        5, 5, 5, 5, 5, 3, 3, 3, 3, 3, 5, 5, 5, 5, 3, 3};
 
 constexpr size_t RED_N = CNT__N + 8 + 64;  // reduce_kernel output slots
 }  // namespace
@@ -119,6 +119,18 @@ const char* mr_fail_message(uint32_t code) {
     case MR_FAIL_KV_GET_WRONG: return "get wrong value";
     case MR_FAIL_KV_MISSING: return "missing element in Append result";
     case MR_FAIL_KV_APPEND_BAD: return "duplicate or wrong order element in Append result";
+    case MR_FAIL_CTRL_NGROUPS: return "assertion failed: c.groups.len() == groups.len()";
+    case MR_FAIL_CTRL_MISSING: return "missing group";
+    case MR_FAIL_CTRL_INVALID: return "shard -> invalid group";
+    case MR_FAIL_CTRL_IMBALANCED: return "imbalanced sharding";
+    case MR_FAIL_CTRL_SERVERS: return "wrong servers for gid";
+    case MR_FAIL_CTRL_HISTORY: return "historical query differs";
+    case MR_FAIL_CTRL_MOVE_NUM: return "Move should increase Tester.Num";
+    case MR_FAIL_CTRL_MOVE_WRONG: return "shard wrong group";
+    case MR_FAIL_CTRL_MINIMAL_JOIN: return "non-minimal transfer after Join()s";
+    case MR_FAIL_CTRL_MINIMAL_LEAVE: return "non-minimal transfer after Leave()s";
+    case MR_FAIL_CTRL_NO_LEADER: return "Leader not found";
+    case MR_FAIL_CTRL_SAME_CONFIG: return "config differs after leader shutdown";
     case MR_FAIL_SIM_CAPACITY: return "simulator capacity exceeded";
     case MR_FAIL_SIM_EVENT_LIMIT: return "simulator event limit exceeded";
     case MR_FAIL_SIM_BAD_PROGRAM: return "scenario program error";
@@ -220,10 +232,14 @@ int mr_batch_create(const mr_cfg* cfg, mr_batch** out) {
   add(&D.stor, C * cfg->apply_cap);
   // scenario-only arrays: spawned tester threads, kvraft servers, churn values
   static const uint8_t k_thr[MR_SCN_COUNT_] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 64,
-                                               0, 4, 4, 0, 0, 0, 0, 0, 0, 6, 6, 6};
+                                               0, 4, 4, 0, 0, 0, 0, 0, 0, 6, 6, 6, 11, 11};
   D.nthr = k_thr[scn];
   if (D.nthr) add(&D.kt32, (size_t)KT__N * D.nthr * C);
-  if (is_kv(scn)) add(&D.kv32, (size_t)KVREC * n * C);
+  if (is_svc(scn)) add(&D.kv32, (size_t)KVREC * n * C);
+  if (is_ctrl(scn)) {
+    add(&D.cfg32, (size_t)CFG_CAP * CFGW * n * C);
+    add(&D.op32, (size_t)OP_CAP * OPW * C);
+  }
   if (is_churn(scn)) {
     add(&D.cval, (size_t)3 * CHURN_VCAP * C);
     add(&D.cidx, (size_t)3 * CHURN_VCAP * C);

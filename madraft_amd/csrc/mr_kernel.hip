@@ -379,8 +379,9 @@ enum : uint32_t { SEND_NONE = 0, SEND_REPLY, SEND_APPEND, SEND_VOTE };
 // (tester.rs:366-396) inlined: committed entries are walked in batches of AC
 // whose loads (log entry, storage mask / value) are all issued before any is
 // used — entries have distinct indices, so a batch never reads what it writes.
-template <bool KV>
+template <uint32_t S>
 DI void node_apply(const Dev& D, X& x, uint32_t me, NC& d, bool& kvready) {
+  constexpr bool KV = is_svc(S);
   const bool snapmode = (x.netmode >> 1) & 1u;
   SE* const sb = D.stor + (size_t)x.c * D.apply_cap;
   uint32_t len = d.slen;
@@ -419,7 +420,10 @@ DI void node_apply(const Dev& D, X& x, uint32_t me, NC& d, bool& kvready) {
         NSV(me) = e[j].val;
         CADD(CNT_SNAPSHOTS, 1u);
       }
-      if constexpr (KV) kv_apply(D, x, me, i, e[j].val, kvready);
+      if constexpr (KV) {
+        kv_apply<is_ctrl(S)>(D, x, me, i, e[j].val, kvready);
+        if (x.code != RUN) return;
+      }
     }
     PROF(P_AP_CHECK);
   }
@@ -473,9 +477,10 @@ DI void ae_load_batch(const Dev& D, const X& x, uint32_t me, const NC& d, uint32
   }
 }
 
-template <bool KV>
+template <uint32_t S>
 DI void node_event(const Dev& D, X& x, bool is_msg, uint32_t tnode, uint32_t slot,
                    uint32_t seq) {
+  constexpr bool KV = is_svc(S);  // kvraft / shard_ctrler request path
   uint32_t me = tnode, src = 0, type = 0, inc = 0, k = 0, mterm = 0, ma = 0, mb = 0, mc = 0;
   bool kvready = false;
   uint32_t hdr_bits = 0;
@@ -665,7 +670,7 @@ DI void node_event(const Dev& D, X& x, bool is_msg, uint32_t tnode, uint32_t slo
     PROF(P_ELECT);
   }
   if (d.applied < d.commit) {  // committed entries reach the tester's applier
-    node_apply<KV>(D, x, me, d, kvready);
+    node_apply<S>(D, x, me, d, kvready);
     if (x.code != RUN) return;
     PROF(P_APPLY);
   }
@@ -745,6 +750,10 @@ DI void t_conn(const Dev& D, X& x, uint32_t i, uint32_t v) {
 DI void t_crash1(const Dev& D, X& x, uint32_t i) {  // tester.rs:329-333
   x.alive &= ~(1u << i);
   set_timer(x, i, INF_T);
+  if (D.kv32) {  // its RPC handler tasks die with it: pending requests are dropped
+    uint4* pp = reinterpret_cast<uint4*>(D.kv32 + ((size_t)x.c * D.n + i) * KVREC + KVR_PEND);
+    for (uint32_t p = 0; p < KV_PEND; p++) pp[p] = make_uint4(0u, 0u, 0u, 0u);
+  }
 }
 DI void t_start1(const Dev& D, X& x, uint32_t i) {  // tester.rs:293-327, raft.rs:108-122
   t_crash1(D, x, i);
@@ -862,7 +871,7 @@ DI void tester(const Dev& D, X& x) {
     if (guard > 4096) { fail(D, x, MR_FAIL_SIM_BAD_PROGRAM); return; }
     if (t.helper != H_NONE) {  // a multi-event tester call in progress
       bool done;
-      if constexpr (is_kv(S)) {
+      if constexpr (is_svc(S)) {
         done = t.helper == H_CALL ? call_step(D, x, t) : join_step(D, x, t);
       } else if constexpr (nthr(S) > 0) {
         done = t.helper == H_ONE    ? one_step(D, x, t)
@@ -969,7 +978,11 @@ __global__ void __launch_bounds__(STEP_BLOCK, MR_WAVES_PER_EU) step_kernel(Dev D
 #endif
     const bool tpick = MR_TESTER_DEN * ns >= MR_TESTER_NUM * (nm + nt + ns);
     const uint32_t pick = tpick ? CLS_TESTER : (nm >= nt ? CLS_MSG : CLS_TIMER);
+#ifdef MR_ALL_CLASSES  // experiment: every lane runs its own event (divergent paths)
+    const bool mine = true;
+#else
     const bool mine = MR_MERGE_NODE ? (tpick ? cls == CLS_TESTER : cls != CLS_TESTER) : cls == pick;
+#endif
     PROF(P_SEL);
     if (!run || !mine) continue;
     if (nthr(S) > 0 && (uint32_t)(key >> 32) == INF_T) {  // nothing can wake the test body
@@ -982,7 +995,7 @@ __global__ void __launch_bounds__(STEP_BLOCK, MR_WAVES_PER_EU) step_kernel(Dev D
     if (x.events > D.max_events) { fail(D, x, MR_FAIL_SIM_EVENT_LIMIT); continue; }
     if (cls != CLS_TESTER) {
       CADD(cls == CLS_MSG ? CNT_EV_MSG : CNT_EV_TIMER, 1u);
-      node_event<is_kv(S)>(D, x, cls == CLS_MSG, node, x.mslot, ((uint32_t)key & 0x3FFFFFFFu) >> 5);
+      node_event<S>(D, x, cls == CLS_MSG, node, x.mslot, ((uint32_t)key & 0x3FFFFFFFu) >> 5);
     } else {
       CADD(CNT_EV_TESTER, 1u);
       if constexpr (nthr(S) > 0) {
@@ -1056,6 +1069,12 @@ __global__ void __launch_bounds__(256) reset_kernel(Dev D) {
     }
     KT(KT_LIVE, 0) = 1u;
   }
+  if (D.cfg32)  // shard_ctrler: every server starts with config 0 (num 0, no groups)
+    for (uint32_t d = 0; d < D.n; d++) {
+      D.kv32[((size_t)x.c * D.n + d) * KVREC + KVR_NCFG] = 1u;
+      uint32_t* c0 = D.cfg32 + (((size_t)x.c * D.n + d) * CFG_CAP) * CFGW;
+      for (uint32_t w = 0; w < CF_GID; w++) c0[w] = 0u;
+    }
 }
 
 // counters_reduce: per-GPU sums / maxima / verdict histogram / first failing

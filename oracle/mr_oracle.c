@@ -46,9 +46,16 @@ enum { KV_OK = 0, KV_WRONG_LEADER = 1, KV_FAILED = 2 };
 #define MAX_CLERKS 16u
 #define KV_SLOTS 6u     /* thread / clerk slots: 0 = main + ck, 1 + cli = client cli */
 #define KV_PEND 8u
+#define CK_SLOTS 16u    /* clerk slots (thread slot k owns clerk k): ck + up to 10 concurrent clerks */
 #define MAX_THR 64u     /* tester thread slots (unreliable_agree_2c: concurrent one() tasks) */
 #define JOIN_ALL 0xFFFFFFFEu
 #define CHURN_VCAP 512u /* values a churn client may record (tests.rs:763-797) */
+/* shard_ctrler (SEMANTICS §10) */
+#define N_SHARDS 10u    /* shard_ctrler/mod.rs:9 */
+#define CFG_CAP 128u    /* configs a controller server may hold */
+#define CFG_G 32u       /* groups in one config */
+#define OP_CAP 256u     /* clerk operations per cluster */
+enum { CT_QUERY = 0, CT_JOIN = 1, CT_LEAVE = 2, CT_MOVE = 3 };
 #define INF_T 0xFFFFFFFFu
 #define LOSS_Q32 429496729u /* floor(0.1 * 2^32), tester.rs:130 */
 
@@ -92,6 +99,11 @@ typedef struct {
   uint64_t cmd; uint32_t t0, starts, index, t1, ph, expected, retry;
 } OThr;
 typedef struct { uint32_t used, idx, clerk, seq, tag, ready, status, value; } OPend;
+/* Config (shard_ctrler/msg.rs:11-18): groups sorted by gid; a server list is
+ * packed as len | a0 << 8 | a1 << 16 | a2 << 24 (addrs! takes `as u8`) */
+typedef struct { uint32_t num, shards[N_SHARDS], ng, gid[CFG_G], addr[CFG_G]; } OCfg;
+/* Op (shard_ctrler/msg.rs:21-37): a = num (Query) / shard (Move), b = gid (Move) */
+typedef struct { uint32_t type, a, b, ng, gid[5], addr[5]; } OOp;
 
 typedef struct {
   mr_cfg cfg;
@@ -109,8 +121,11 @@ typedef struct {
   uint32_t kv_mode, kv_done, next_tid, mwake, main_join;
   uint32_t kv_n[MR_MAX_NODES][8], kv_ok[MR_MAX_NODES], kv_dedup[MR_MAX_NODES][MAX_CLERKS];
   OPend pend[MR_MAX_NODES][KV_PEND];
-  OClerk ck[KV_SLOTS]; OThr th[MAX_THR];
+  OClerk ck[CK_SLOTS]; OThr th[MAX_THR];
   uint64_t* cval; uint32_t* cidx; /* churn values [3][CHURN_VCAP] + their indices */
+  uint32_t ctrl_mode, nops, ncfg[MR_MAX_NODES];
+  OCfg* cfgs; /* [MR_MAX_NODES][CFG_CAP] */
+  OOp* ops;   /* [OP_CAP] */
   uint32_t churn_stop;
   /* results */
   mro_result r;
@@ -214,7 +229,7 @@ static void reset_timer(OSim* s, uint32_t d) {
 static int host_conn(OSim* s, uint32_t h) { return h < CLERK_HOST ? s->nd[h].conn : 1; }
 static uint32_t* host_nctr(OSim* s, uint32_t h) {
   if (h < CLERK_HOST) return &s->nd[h].n_ctr;
-  for (uint32_t k = 0; k < KV_SLOTS; k++)
+  for (uint32_t k = 0; k < CK_SLOTS; k++)
     if (s->ck[k].id == h - CLERK_HOST) return &s->ck[k].nctr;
   t_fail(s, MR_FAIL_SIM_BAD_PROGRAM);
   return NULL;
@@ -288,12 +303,88 @@ static void log_put(OSim* s, ONode* d, uint32_t i, uint32_t t, uint64_t v) {
 
 /* kvraft Server::apply + Kv::apply (the build's completion of kvraft/server.rs:68-87,
  * SEMANTICS §9): dedup by (clerk, seq), value model (n, ok), answer pending requests */
+/* the build's rebalance (SEMANTICS §10): every shard assigned, group loads
+ * differ by <= 1, and a shard only moves off a removed or over-target group */
+static void ctl_rebalance(OCfg* c) {
+  if (c->ng == 0) { for (uint32_t j = 0; j < N_SHARDS; j++) c->shards[j] = 0; return; }
+  uint32_t cnt[CFG_G], tgt[CFG_G], pool[N_SHARDS], np = 0, rank[CFG_G];
+  for (uint32_t g = 0; g < c->ng; g++) cnt[g] = 0;
+  for (uint32_t j = 0; j < N_SHARDS; j++) {
+    uint32_t g = 0;
+    while (g < c->ng && c->gid[g] != c->shards[j]) g++;
+    if (g < c->ng) cnt[g]++;
+    else c->shards[j] = 0;
+  }
+  /* targets: base + 1 for the `extra` groups with the most shards (ties: smaller gid) */
+  uint32_t base = N_SHARDS / c->ng, extra = N_SHARDS % c->ng;
+  for (uint32_t g = 0; g < c->ng; g++) {
+    rank[g] = 0;
+    for (uint32_t h = 0; h < c->ng; h++)
+      if (cnt[h] > cnt[g] || (cnt[h] == cnt[g] && h < g)) rank[g]++;
+    tgt[g] = base + (rank[g] < extra ? 1u : 0u);
+  }
+  for (uint32_t g = 0; g < c->ng; g++) /* release over-target shards, highest shard first */
+    for (int j = N_SHARDS - 1; j >= 0 && cnt[g] > tgt[g]; j--)
+      if (c->shards[j] == c->gid[g]) { c->shards[j] = 0; cnt[g]--; }
+  for (uint32_t j = 0; j < N_SHARDS; j++)
+    if (c->shards[j] == 0) pool[np++] = j;
+  for (uint32_t k = 0; k < np; k++) { /* unassigned shards, ascending, to the first group below target */
+    uint32_t g = 0;
+    while (cnt[g] >= tgt[g]) g++;
+    c->shards[pool[k]] = c->gid[g];
+    cnt[g]++;
+  }
+}
+
+/* ShardInfo::apply (the build's completion of shard_ctrler/server.rs:8-19) at server me;
+ * returns the output: for a Query the index of the answered config in me's store */
+static uint32_t ctl_apply(OSim* s, uint32_t me, uint32_t clerk, uint32_t seq, uint32_t op_id) {
+  const OOp* op = &s->ops[op_id];
+  OCfg* store = &s->cfgs[me * CFG_CAP];
+  uint32_t nc = s->ncfg[me];
+  if (op->type == CT_QUERY) return op->a >= nc ? nc - 1 : op->a;
+  if (seq <= s->kv_dedup[me][clerk]) return 0; /* duplicate */
+  s->kv_dedup[me][clerk] = seq;
+  if (nc >= CFG_CAP) t_fail(s, MR_FAIL_SIM_CAPACITY);
+  OCfg* c = &store[nc];
+  *c = store[nc - 1];
+  c->num = nc;
+  if (op->type == CT_JOIN) {
+    for (uint32_t k = 0; k < op->ng; k++) {
+      uint32_t g = 0;
+      while (g < c->ng && c->gid[g] < op->gid[k]) g++;
+      if (g < c->ng && c->gid[g] == op->gid[k]) { c->addr[g] = op->addr[k]; continue; }
+      if (c->ng >= CFG_G) t_fail(s, MR_FAIL_SIM_CAPACITY);
+      for (uint32_t h = c->ng; h > g; h--) { c->gid[h] = c->gid[h - 1]; c->addr[h] = c->addr[h - 1]; }
+      c->gid[g] = op->gid[k]; c->addr[g] = op->addr[k]; c->ng++;
+    }
+    ctl_rebalance(c);
+  } else if (op->type == CT_LEAVE) {
+    for (uint32_t k = 0; k < op->ng; k++) {
+      uint32_t g = 0;
+      while (g < c->ng && c->gid[g] != op->gid[k]) g++;
+      if (g == c->ng) continue;
+      for (uint32_t h = g; h + 1 < c->ng; h++) { c->gid[h] = c->gid[h + 1]; c->addr[h] = c->addr[h + 1]; }
+      c->ng--;
+    }
+    ctl_rebalance(c);
+  } else {
+    if (op->a < N_SHARDS) c->shards[op->a] = op->b;
+  }
+  s->ncfg[me] = nc + 1;
+  return 0;
+}
+
 static void kv_apply(OSim* s, uint32_t me, uint32_t i, uint64_t v) {
   uint32_t op = (uint32_t)(v >> 56) & 3u, key = (uint32_t)(v >> 53) & 7u;
   uint32_t clerk = (uint32_t)(v >> 48) & 31u, seq = (uint32_t)(v >> 24) & 0xFFFFFFu;
   uint32_t elem = (uint32_t)v & 0xFFFFFFu, out = 0;
   uint32_t* n = &s->kv_n[me][key];
-  if (op == KV_GET) {
+  int query = op == KV_GET;
+  if (s->ctrl_mode) { /* shard_ctrler: elem = the operation's id */
+    out = ctl_apply(s, me, clerk, seq, elem);
+    query = s->ops[elem].type == CT_QUERY;
+  } else if (op == KV_GET) {
     out = *n | (((s->kv_ok[me] >> key) & 1u) << 31);
   } else if (seq > s->kv_dedup[me][clerk]) {
     if (op == KV_PUT) { *n = 0; s->kv_ok[me] |= 1u << key; }
@@ -305,7 +396,7 @@ static void kv_apply(OSim* s, uint32_t me, uint32_t i, uint64_t v) {
     OPend* q = &s->pend[me][p];
     if (!q->used || q->ready || q->idx != i) continue;
     int ok = q->clerk == clerk && q->seq == seq;
-    q->ready = 1; q->status = ok ? KV_OK : KV_FAILED; q->value = (ok && op == KV_GET) ? out : 0;
+    q->ready = 1; q->status = ok ? KV_OK : KV_FAILED; q->value = (ok && query) ? out : 0;
   }
 }
 
@@ -323,7 +414,7 @@ static void kv_flush(OSim* s, uint32_t me) {
     OPend* q = &s->pend[me][p];
     if (!q->used || !q->ready) continue;
     q->used = 0; q->ready = 0;
-    kv_send_rep(s, me, CLERK_HOST + q->clerk, q->tag, q->status, 0, q->value);
+    kv_send_rep(s, me, CLERK_HOST + q->clerk, q->tag, q->status, me, q->value); /* hint = server */
   }
 }
 
@@ -422,7 +513,7 @@ static void clerk_deliver(OSim* s, OMsg* m) {
   uint32_t id = m->dst - CLERK_HOST;
   OClerk* c = NULL;
   uint32_t slot = 0;
-  for (uint32_t k = 0; k < KV_SLOTS; k++)
+  for (uint32_t k = 0; k < CK_SLOTS; k++)
     if (s->th[k].live && s->ck[k].id == id) { c = &s->ck[k]; slot = k; }
   if (!host_conn(s, m->src)) { s->r.drop_deliver++; rec_host(s, 16, m->dst, m->seq); return; }
   if (!c || !c->waiting || c->got || m->term != c->tag) {
@@ -679,6 +770,7 @@ static void t_disconnect(OSim* s, uint32_t i) { s->nd[i].conn = 0; }
 
 static void t_crash1(OSim* s, uint32_t i) { /* tester.rs:329-333 */
   ONode* d = &s->nd[i];
+  memset(s->pend[i], 0, sizeof s->pend[i]); /* its RPC handler tasks die with it */
   d->alive = 0;
   d->timer_gen++;
 }
@@ -1345,11 +1437,15 @@ static void one_thr_step(OSim* s, uint32_t slot) {
   }
 }
 
+static void ctl_client_step(OSim* s, uint32_t slot);
+
 static void client_step(OSim* s, uint32_t slot) {
   switch (s->scenario) {
     case MR_SCN_RELIABLE_CHURN_2C:
     case MR_SCN_UNRELIABLE_CHURN_2C: churn_step(s, slot); break;
     case MR_SCN_UNRELIABLE_AGREE_2C: one_thr_step(s, slot); break;
+    case MR_SCN_CTRL_BASIC_4A:
+    case MR_SCN_CTRL_MULTI_4A: ctl_client_step(s, slot); break;
     default: kv_client_step(s, slot); break;
   }
 }
@@ -1489,6 +1585,227 @@ static void scn_kv_generic(OSim* s, uint32_t nclients, int unreliable) { /* kvra
   t_end(s);
 }
 
+/* ---- shard_ctrler tests (src/shard_ctrler/tests.rs, tester.rs; SEMANTICS §10) ---- */
+static uint32_t ct_op(OSim* s, uint32_t type, uint32_t a, uint32_t b) {
+  if (s->nops >= OP_CAP) t_fail(s, MR_FAIL_SIM_CAPACITY);
+  OOp* op = &s->ops[s->nops];
+  memset(op, 0, sizeof *op);
+  op->type = type; op->a = a; op->b = b;
+  return s->nops++;
+}
+static void ct_grp(OSim* s, uint32_t id, uint32_t gid, uint32_t addr) { /* groups! / gids entry */
+  OOp* op = &s->ops[id];
+  op->gid[op->ng] = gid; op->addr[op->ng] = addr; op->ng++;
+}
+static uint32_t addrs(uint32_t n, uint32_t a0, uint32_t a1, uint32_t a2) { /* addrs![..], `as u8` */
+  return n | (a0 & 255u) << 8 | (n > 1 ? (a1 & 255u) << 16 : 0) | (n > 2 ? (a2 & 255u) << 24 : 0);
+}
+/* ck.<op>() by the test body: the reply's config (Query) as (server, index) */
+static const OCfg* ct_call(OSim* s, uint32_t id) {
+  uint32_t idx = main_call(s, 0, 0, id);
+  return &s->cfgs[s->ck[0].rhint * CFG_CAP + idx];
+}
+static const OCfg* ct_query(OSim* s, uint32_t num) { return ct_call(s, ct_op(s, CT_QUERY, num, 0)); }
+static int cfg_has(const OCfg* c, uint32_t gid) {
+  for (uint32_t g = 0; g < c->ng; g++) if (c->gid[g] == gid) return 1;
+  return 0;
+}
+static int cfg_eq(const OCfg* a, const OCfg* b) {
+  if (a->num != b->num || a->ng != b->ng) return 0;
+  for (uint32_t j = 0; j < N_SHARDS; j++) if (a->shards[j] != b->shards[j]) return 0;
+  for (uint32_t g = 0; g < a->ng; g++)
+    if (a->gid[g] != b->gid[g] || a->addr[g] != b->addr[g]) return 0;
+  return 1;
+}
+static void ct_servers(OSim* s, const OCfg* c, uint32_t gid, uint32_t addr) { /* cfx.groups[&gid] == addr */
+  for (uint32_t g = 0; g < c->ng; g++)
+    if (c->gid[g] == gid) { if (c->addr[g] != addr) t_fail(s, MR_FAIL_CTRL_SERVERS); return; }
+  t_fail(s, MR_FAIL_CTRL_SERVERS); /* HashMap index panics */
+}
+static void ct_check(OSim* s, uint32_t ng, const uint32_t* gids) { /* Clerk::check, tester.rs:113-150 */
+  const OCfg* c = ct_query(s, 0xFFFFFFFFu);
+  if (c->ng != ng) t_fail(s, MR_FAIL_CTRL_NGROUPS);
+  for (uint32_t k = 0; k < ng; k++) if (!cfg_has(c, gids[k])) t_fail(s, MR_FAIL_CTRL_MISSING);
+  if (ng == 0)
+    for (uint32_t j = 0; j < N_SHARDS; j++)
+      if (c->shards[j] != 0 && !cfg_has(c, c->shards[j])) t_fail(s, MR_FAIL_CTRL_INVALID);
+  if (c->ng) {
+    uint32_t mn = ~0u, mx = 0;
+    for (uint32_t g = 0; g < c->ng; g++) {
+      uint32_t k = 0;
+      for (uint32_t j = 0; j < N_SHARDS; j++) k += c->shards[j] == c->gid[g];
+      if (k < mn) mn = k;
+      if (k > mx) mx = k;
+    }
+    if (mx > mn + 1) t_fail(s, MR_FAIL_CTRL_IMBALANCED);
+  }
+}
+static void ct_minimal(OSim* s, const OCfg* a, const OCfg* b, uint32_t npara, uint32_t code) {
+  for (uint32_t i = 1; i <= npara; i++) /* tests.rs:133-140 / 152-159 */
+    for (uint32_t j = 0; j < N_SHARDS; j++)
+      if (b->shards[j] == i && a->shards[j] != i) t_fail(s, code);
+}
+static int ct_leader(OSim* s) { /* Tester::leader, shard_ctrler/tester.rs:76-87 */
+  for (uint32_t i = 0; i < s->n; i++) if (s->nd[i].alive && s->nd[i].role == R_L) return (int)i;
+  return -1;
+}
+
+/* a concurrent client task (tests.rs:110-117 / 224-233): one clerk call per segment chain */
+static void ctl_client_step(OSim* s, uint32_t slot) {
+  OThr* t = &s->th[slot];
+  const uint32_t gid = t->cli, multi = s->scenario == MR_SCN_CTRL_MULTI_4A;
+  const uint32_t nops = multi ? 2 : 3;
+  if (t->pc > 0 && !clerk_resume(s, slot)) goto block; /* the call in flight */
+  if (t->pc == nops) { rec_simple(s, 2, t->tid & 0xFFu); thr_finish(s, slot); return; }
+  {
+    uint32_t id;
+    if (!multi) {
+      if (t->pc == 0) { id = ct_op(s, CT_JOIN, 0, 0); ct_grp(s, id, gid + 1000, addrs(1, gid + 1, 0, 0)); }
+      else if (t->pc == 1) { id = ct_op(s, CT_JOIN, 0, 0); ct_grp(s, id, gid, addrs(1, gid + 2, 0, 0)); }
+      else { id = ct_op(s, CT_LEAVE, 0, 0); ct_grp(s, id, gid + 1000, 0); }
+    } else if (t->pc == 0) {
+      id = ct_op(s, CT_JOIN, 0, 0);
+      ct_grp(s, id, gid, addrs(3, gid + 1, gid + 2, gid + 3));
+      ct_grp(s, id, gid + 1000, addrs(1, gid + 1000 + 1, 0, 0));
+      ct_grp(s, id, gid + 2000, addrs(1, gid + 2000 + 1, 0, 0));
+    } else {
+      id = ct_op(s, CT_LEAVE, 0, 0);
+      ct_grp(s, id, gid + 1000, 0); ct_grp(s, id, gid + 2000, 0);
+    }
+    t->pc++;
+    clerk_begin(s, slot, 0, 0, id);
+  }
+block:
+  rec_simple(s, 2, t->tid & 0xFFu);
+}
+
+static void ct_spawn(OSim* s, uint32_t slot, uint32_t tid, uint32_t gid) {
+  thr_spawn(s, slot, tid);
+  s->th[slot].cli = gid;
+  memset(&s->ck[slot], 0, sizeof s->ck[slot]);
+  s->ck[slot].id = tid; /* cka = t.make_client() */
+}
+
+static void scn_ctrl_basic(OSim* s) { /* basic_4a, shard_ctrler/tests.rs:24-166 */
+  const uint32_t npara = 10;
+  const OCfg* cfa[8];
+  uint32_t ncfa = 0, id, g[10];
+  t_new(s, 0);
+  s->kv_mode = 1; s->ctrl_mode = 1; s->th[0].live = 1;
+  cfa[ncfa++] = ct_query(s, 0xFFFFFFFFu);
+  ct_check(s, 0, g);
+  id = ct_op(s, CT_JOIN, 0, 0); ct_grp(s, id, 1, addrs(3, 11, 12, 13)); ct_call(s, id);
+  g[0] = 1; ct_check(s, 1, g);
+  cfa[ncfa++] = ct_query(s, 0xFFFFFFFFu);
+  id = ct_op(s, CT_JOIN, 0, 0); ct_grp(s, id, 2, addrs(3, 21, 22, 23)); ct_call(s, id);
+  g[1] = 2; ct_check(s, 2, g);
+  cfa[ncfa++] = ct_query(s, 0xFFFFFFFFu);
+  const OCfg* cfx = ct_query(s, 0xFFFFFFFFu);
+  ct_servers(s, cfx, 1, addrs(3, 11, 12, 13));
+  ct_servers(s, cfx, 2, addrs(3, 21, 22, 23));
+  id = ct_op(s, CT_LEAVE, 0, 0); ct_grp(s, id, 1, 0); ct_call(s, id);
+  g[0] = 2; ct_check(s, 1, g);
+  cfa[ncfa++] = ct_query(s, 0xFFFFFFFFu);
+  id = ct_op(s, CT_LEAVE, 0, 0); ct_grp(s, id, 2, 0); ct_call(s, id);
+  cfa[ncfa++] = ct_query(s, 0xFFFFFFFFu);
+  for (uint32_t sv = 0; sv < s->n; sv++) { /* Historical queries */
+    t_crash1(s, sv);
+    for (uint32_t k = 0; k < ncfa; k++)
+      if (!cfg_eq(ct_query(s, cfa[k]->num), cfa[k])) t_fail(s, MR_FAIL_CTRL_HISTORY);
+    t_start1(s, sv);
+  }
+  id = ct_op(s, CT_JOIN, 0, 0); ct_grp(s, id, 503, addrs(3, 31, 32, 33)); ct_call(s, id);
+  id = ct_op(s, CT_JOIN, 0, 0); ct_grp(s, id, 504, addrs(3, 41, 42, 43)); ct_call(s, id);
+  for (uint32_t i = 0; i < N_SHARDS; i++) { /* Move */
+    const OCfg* cf = ct_query(s, 0xFFFFFFFFu);
+    uint32_t shard = i < N_SHARDS / 2 ? 503 : 504;
+    ct_call(s, ct_op(s, CT_MOVE, i, shard));
+    if (cf->shards[i] != shard) {
+      const OCfg* cf1 = ct_query(s, 0xFFFFFFFFu);
+      if (!(cf1->num > cf->num)) t_fail(s, MR_FAIL_CTRL_MOVE_NUM);
+    }
+  }
+  const OCfg* cf2 = ct_query(s, 0xFFFFFFFFu);
+  for (uint32_t i = 0; i < N_SHARDS; i++)
+    if (cf2->shards[i] != (i < N_SHARDS / 2 ? 503u : 504u)) t_fail(s, MR_FAIL_CTRL_MOVE_WRONG);
+  id = ct_op(s, CT_LEAVE, 0, 0); ct_grp(s, id, 503, 0); ct_call(s, id);
+  id = ct_op(s, CT_LEAVE, 0, 0); ct_grp(s, id, 504, 0); ct_call(s, id);
+  for (uint32_t i = 0; i < npara; i++) ct_spawn(s, 1 + i, 1 + i, i * 10 + 100); /* Concurrent leave/join */
+  t_join_all(s);
+  for (uint32_t i = 0; i < npara; i++) g[i] = i * 10 + 100;
+  ct_check(s, npara, g);
+  const OCfg* c1 = ct_query(s, 0xFFFFFFFFu); /* Minimal transfers after joins */
+  for (uint32_t i = 0; i < 5; i++) {
+    uint32_t gid = npara + 1 + i;
+    id = ct_op(s, CT_JOIN, 0, 0); ct_grp(s, id, gid, addrs(3, gid + 1, gid + 2, gid + 2)); ct_call(s, id);
+  }
+  const OCfg* c2 = ct_query(s, 0xFFFFFFFFu);
+  ct_minimal(s, c1, c2, npara, MR_FAIL_CTRL_MINIMAL_JOIN);
+  for (uint32_t i = 0; i < 5; i++) { /* Minimal transfers after leaves */
+    id = ct_op(s, CT_LEAVE, 0, 0); ct_grp(s, id, npara + 1 + i, 0); ct_call(s, id);
+  }
+  const OCfg* c3 = ct_query(s, 0xFFFFFFFFu);
+  ct_minimal(s, c3, c2, npara, MR_FAIL_CTRL_MINIMAL_LEAVE); /* !(c2 == i && c3 != i) */
+  t_end(s);
+}
+
+static void scn_ctrl_multi(OSim* s) { /* multi_4a, shard_ctrler/tests.rs:168-299 */
+  const uint32_t npara = 10;
+  uint32_t id, g[10];
+  t_new(s, 0);
+  s->kv_mode = 1; s->ctrl_mode = 1; s->th[0].live = 1;
+  ct_query(s, 0xFFFFFFFFu); /* cfa.push */
+  ct_check(s, 0, g);
+  id = ct_op(s, CT_JOIN, 0, 0);
+  ct_grp(s, id, 1, addrs(3, 11, 12, 13)); ct_grp(s, id, 2, addrs(3, 21, 22, 23)); ct_call(s, id);
+  g[0] = 1; g[1] = 2; ct_check(s, 2, g);
+  ct_query(s, 0xFFFFFFFFu);
+  id = ct_op(s, CT_JOIN, 0, 0); ct_grp(s, id, 3, addrs(3, 31, 32, 33)); ct_call(s, id);
+  g[2] = 3; ct_check(s, 3, g);
+  ct_query(s, 0xFFFFFFFFu);
+  const OCfg* cfx = ct_query(s, 0xFFFFFFFFu);
+  ct_servers(s, cfx, 1, addrs(3, 11, 12, 13));
+  ct_servers(s, cfx, 2, addrs(3, 21, 22, 23));
+  ct_servers(s, cfx, 3, addrs(3, 31, 32, 33));
+  id = ct_op(s, CT_LEAVE, 0, 0); ct_grp(s, id, 1, 0); ct_grp(s, id, 3, 0); ct_call(s, id);
+  g[0] = 2; ct_check(s, 1, g);
+  ct_query(s, 0xFFFFFFFFu);
+  cfx = ct_query(s, 0xFFFFFFFFu);
+  ct_servers(s, cfx, 2, addrs(3, 21, 22, 23));
+  id = ct_op(s, CT_LEAVE, 0, 0); ct_grp(s, id, 2, 0); ct_call(s, id);
+  for (uint32_t i = 0; i < npara; i++) ct_spawn(s, 1 + i, 1 + i, i + 1000); /* Concurrent multi leave/join */
+  t_join_all(s);
+  for (uint32_t i = 0; i < npara; i++) g[i] = i + 1000;
+  ct_check(s, npara, g);
+  const OCfg* c1 = ct_query(s, 0xFFFFFFFFu); /* Minimal transfers after multijoins */
+  id = ct_op(s, CT_JOIN, 0, 0);
+  for (uint32_t i = 0; i < 5; i++) {
+    uint32_t gid = npara + 1 + i;
+    ct_grp(s, id, gid, addrs(2, gid + 1, gid + 2, 0));
+  }
+  ct_call(s, id);
+  const OCfg* c2 = ct_query(s, 0xFFFFFFFFu);
+  ct_minimal(s, c1, c2, npara, MR_FAIL_CTRL_MINIMAL_JOIN);
+  id = ct_op(s, CT_LEAVE, 0, 0); /* Minimal transfers after multileaves */
+  for (uint32_t i = 0; i < 5; i++) ct_grp(s, id, npara + 1 + i, 0);
+  ct_call(s, id);
+  const OCfg* c3 = ct_query(s, 0xFFFFFFFFu);
+  ct_minimal(s, c3, c2, npara, MR_FAIL_CTRL_MINIMAL_LEAVE);
+  int leader = ct_leader(s); /* Check Same config on servers */
+  if (leader < 0) t_fail(s, MR_FAIL_CTRL_NO_LEADER);
+  const OCfg* c = ct_query(s, 0xFFFFFFFFu);
+  t_crash1(s, (uint32_t)leader);
+  uint32_t attempts = 0;
+  while (ct_leader(s) >= 0) {
+    attempts++;
+    if (!(attempts < 3)) t_fail(s, MR_FAIL_CTRL_NO_LEADER);
+    t_sleep(s, 1000000u);
+  }
+  const OCfg* c1b = ct_query(s, 0xFFFFFFFFu);
+  if (!cfg_eq(c, c1b)) t_fail(s, MR_FAIL_CTRL_SAME_CONFIG);
+  t_end(s);
+}
+
 static int run_scenario(OSim* s) {
   switch (s->scenario) {
     case MR_SCN_INITIAL_ELECTION_2A: scn_initial_election(s); break;
@@ -1515,6 +1832,8 @@ static int run_scenario(OSim* s) {
     case MR_SCN_UNRELIABLE_AGREE_2C: scn_unreliable_agree(s); break;
     case MR_SCN_RELIABLE_CHURN_2C: scn_churn(s, 0); break;
     case MR_SCN_UNRELIABLE_CHURN_2C: scn_churn(s, 1); break;
+    case MR_SCN_CTRL_BASIC_4A: scn_ctrl_basic(s); break;
+    case MR_SCN_CTRL_MULTI_4A: scn_ctrl_multi(s); break;
     case MR_SCN_KV_BASIC_3A: scn_kv_generic(s, 1, 0); break;
     case MR_SCN_KV_CONCURRENT_3A: scn_kv_generic(s, 5, 0); break;
     case MR_SCN_KV_UNRELIABLE_3A: scn_kv_generic(s, 5, 1); break;
@@ -1538,6 +1857,8 @@ static int sim_alloc(OSim* s, const mr_cfg* cfg) {
     s->nd[i].lterm = (uint32_t*)malloc(cfg->log_cap * sizeof(uint32_t));
     s->nd[i].lval = (uint64_t*)malloc(cfg->log_cap * sizeof(uint64_t));
   }
+  s->cfgs = (OCfg*)malloc(MR_MAX_NODES * CFG_CAP * sizeof(OCfg));
+  s->ops = (OOp*)malloc(OP_CAP * sizeof(OOp));
   s->cval = (uint64_t*)malloc(3 * CHURN_VCAP * sizeof(uint64_t));
   s->cidx = (uint32_t*)malloc(3 * CHURN_VCAP * sizeof(uint32_t));
   s->mask = (uint8_t*)malloc(cfg->apply_cap);
@@ -1548,6 +1869,7 @@ static int sim_alloc(OSim* s, const mr_cfg* cfg) {
 static void sim_free(OSim* s) {
   for (uint32_t i = 0; i < MR_MAX_NODES; i++) { free(s->nd[i].lterm); free(s->nd[i].lval); }
   free(s->mask); free(s->sval); free(s->heap); free(s->cval); free(s->cidx);
+  free(s->cfgs); free(s->ops);
 }
 
 static void sim_reset(OSim* s, uint64_t cluster) {
@@ -1571,6 +1893,11 @@ static void sim_reset(OSim* s, uint64_t cluster) {
   memset(s->kv_n, 0, sizeof s->kv_n); memset(s->kv_ok, 0, sizeof s->kv_ok);
   memset(s->kv_dedup, 0, sizeof s->kv_dedup); memset(s->pend, 0, sizeof s->pend);
   memset(s->ck, 0, sizeof s->ck); memset(s->th, 0, sizeof s->th); s->churn_stop = 0;
+  s->ctrl_mode = 0; s->nops = 0;
+  for (uint32_t i = 0; i < MR_MAX_NODES; i++) { /* the initial config, num 0 */
+    s->ncfg[i] = 1;
+    memset(&s->cfgs[i * CFG_CAP], 0, sizeof(OCfg));
+  }
   memset(s->mask, 0, s->cfg.apply_cap);
   for (uint32_t i = 0; i < MR_MAX_NODES; i++) s->slen[i] = 1;
   memset(&s->r, 0, sizeof s->r);
@@ -1641,7 +1968,7 @@ static const char* k_names[MR_SCN_COUNT_] = {
     "unreliable_churn_2c", "snapshot_basic_2d", "snapshot_install_2d",
     "snapshot_install_unreliable_2d", "snapshot_install_crash_2d",
     "snapshot_install_unreliable_crash_2d", "figure_8_unreliable_crash", "basic_3a",
-    "concurrent_3a", "unreliable_3a"};
+    "concurrent_3a", "unreliable_3a", "basic_4a", "multi_4a"};
 
 uint32_t mro_scenario_from_name(const char* name) {
   for (uint32_t i = 1; i < MR_SCN_COUNT_; i++)
@@ -1651,7 +1978,7 @@ uint32_t mro_scenario_from_name(const char* name) {
 
 int mro_cfg_init(mr_cfg* c, uint32_t scn) {
   static const uint8_t k_n[MR_SCN_COUNT_] = {0, 3, 3, 7, 5, 3, 5, 3, 3, 5, 3, 3, 5, 3,
-                                             5, 5, 5, 5, 5, 3, 3, 3, 3, 3, 5, 5, 5, 5};
+                                             5, 5, 5, 5, 5, 3, 3, 3, 3, 3, 5, 5, 5, 5, 3, 3};
   if (scn == 0 || scn >= MR_SCN_COUNT_) return -1;
   memset(c, 0, sizeof *c);
   c->abi_version = MR_ABI_VERSION;

@@ -2,5 +2,5 @@
 # bench each library variant under madraft_amd/lib/var/ (dev tool)
 for f in "$@"; do
   MADRAFT_HIP_LIB=$PWD/madraft_amd/lib/var/$f timeout -k 10 300 python bench.py --steps 2 --warmup 1 --no-cpu-baseline > gpurun_out/bench_$f.log 2>&1 || { echo "$f FAILED"; tail -3 gpurun_out/bench_$f.log; continue; }
-  python -c "import json; d=json.loads(open('gpurun_out/bench_$f.log').read().strip().splitlines()[-1]); print('$f', d['value'], d['ms_per_step'], d['roofline']['frac'], d['roofline']['launches_per_step'])"
+  python -c "import json; d=json.loads(open('gpurun_out/bench_$f.log').read().strip().splitlines()[-1]); print('$f', d['value'], d['ms_per_step'], d['roofline']['frac'], d['roofline']['launches'])"
 done
