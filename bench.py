@@ -85,15 +85,20 @@ def main():
     ap.add_argument("--test", default="figure_8_unreliable_2c")
     ap.add_argument("--cpu-seeds", type=int, default=20000, help="cpu_baseline seeds per process")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--dist-backend", default="nccl", help="nccl (RCCL) or gloo (one-GPU rehearsal)")
     a = ap.parse_args()
 
     rank = int(os.environ.get("RANK", 0))
     world = int(os.environ.get("WORLD_SIZE", 1))
-    local = int(os.environ.get("LOCAL_RANK", 0))
+    local = int(os.environ.get("LOCAL_RANK", 0)) % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)  # RCCL over xGMI
+        if a.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)  # RCCL over xGMI
+        else:  # rehearsal of the N>1 path on one GPU (tests): counters all-reduced on the host
+            dist.init_process_group(a.dist_backend)
+            dev = torch.device("cpu")
 
     def barrier():
         if world > 1:

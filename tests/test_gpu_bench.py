@@ -1,0 +1,45 @@
+"""GPU: bench.py's contract on one MI355X — the single-rank JSON line, and the
+N>1 path (two ranks sharing the card, counters all-reduced over gloo) giving
+the same whole-job totals as one rank over the same clusters."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _run(args, timeout=240):
+    r = subprocess.run(args, cwd=ROOT, capture_output=True, text=True, timeout=timeout)
+    assert r.returncode == 0, r.stderr[-2000:]
+    return json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+
+
+def test_bench_single_rank_json():
+    d = _run([sys.executable, "bench.py", "--steps", "1", "--warmup", "0", "--clusters", "4096",
+              "--no-cpu-baseline"])
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
+              "higher_is_better", "scaling", "vs_baseline", "dtype", "data", "config", "roofline"):
+        assert k in d, k
+    assert d["n_gpus"] == 1 and d["config"]["clusters_total"] == 4096
+    assert d["value"] > 0 and d["pass_rate"] > 0.99
+    assert d["roofline"]["bound"] == "hbm" and 0 < d["roofline"]["frac"] < 1
+
+
+def test_bench_two_ranks_one_gpu():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    d = _run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+              "--master-addr", "127.0.0.1", "--master-port", str(port), "bench.py", "--gpus", "2",
+              "--steps", "1", "--warmup", "0", "--clusters", "2048", "--dist-backend", "gloo"])
+    assert d["n_gpus"] == 2 and d["config"]["clusters_total"] == 4096
+    assert d["scaling"] == "weak" and d["value"] > 0 and d["pass_rate"] > 0.99
+    one = _run([sys.executable, "bench.py", "--steps", "1", "--warmup", "0", "--clusters", "4096",
+                "--no-cpu-baseline"])
+    # same seeds (global cluster ids), so the same events whatever the rank count
+    assert d["events_per_seed"] == one["events_per_seed"]
