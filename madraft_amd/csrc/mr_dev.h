@@ -51,12 +51,15 @@ enum : uint32_t {
 };
 // cs64 [C64__N][C]: per-cluster u64 scalars
 enum : uint32_t { C64_FREE, C64_DIGEST, C64_MMIN, C64_THV, C64_TV, C64__N = C64_TV + T_NV };
-// nd32 [C][n][NREC]: one 128-B record per node. Words 0..10 are the scalars
-// an event loads / stores as a block (load_node), 11..13 the rest, 14..15 the
-// snapshot value (u64), 16..23 next[p], 24..31 match[p] (leader -> peer p).
+// nd32 [C][n][NREC]: one 128-B record per node. Words 0..11 are the scalars
+// an event loads / stores as a block (load_node), 12..13 the pending payload
+// range, 14..15 the snapshot value (u64), 16..23 next[p], 24..31 match[p]
+// (leader -> peer p). match[me] holds the leader's base: its last index when it
+// won its term (every entry above it, and none at or below, has the current
+// term). LASTT caches term_at(last). Node timers live in tmr [n][C].
 enum : uint32_t {
   NF_FLAGS, NF_TERM, NF_COMMIT, NF_APPLIED, NF_LAST, NF_SNAP, NF_SNAPT, NF_ECTR, NF_NCTR,
-  NF_PEXP, NF_SLEN, NF_TIMER, NF_PLO, NF_PHI, NF_SNAPV, NF__N = 16
+  NF_PEXP, NF_SLEN, NF_LASTT, NF_PLO, NF_PHI, NF_SNAPV, NF__N = 16
 };
 enum : uint32_t { PF_NEXT, PF_MATCH, PF__N };
 constexpr uint32_t NR_PEER = 16;  // next[] at 16, match[] at 16 + MR_MAX_NODES
@@ -118,6 +121,7 @@ struct Dev {
   uint32_t* cs32;
   uint64_t* cs64;
   uint32_t* nd32;   // [C][n][NREC]
+  uint32_t* tmr;    // [n][C] node timers (registers during a launch)
   uint32_t* ms32;   // [C][M][MREC]
   uint64_t* mkey;   // [M][C]
   LE* log;  // [C][n][log_cap] ring per node

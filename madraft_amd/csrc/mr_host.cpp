@@ -225,6 +225,7 @@ int mr_batch_create(const mr_cfg* cfg, mr_batch** out) {
   add(&D.cs32, (size_t)CS__N * C);
   add(&D.cs64, (size_t)C64__N * C);
   add(&D.nd32, (size_t)NREC * n * C);
+  add(&D.tmr, n * C);
   add(&D.ms32, (size_t)MREC * M * C);
   add(&D.mkey, (size_t)M * C);
   add(&D.log, C * n * cfg->log_cap);

@@ -58,6 +58,7 @@ struct X {
 #define MS32(f, s) MSP(s)[f]
 #define MSV(s) (*reinterpret_cast<uint64_t*>(MSP(s) + MF_V))
 #define MKEY(s) D.mkey[(size_t)(s) * D.C + x.c]
+#define TMR(d) D.tmr[(size_t)(d) * D.C + x.c]
 // message keys of the lane's cluster live in LDS during a launch: [slot][lane],
 // so a wave's 64 lanes read 64 consecutive u64 (conflict-free). Free slots hold
 // ~0, so the earliest-message scan is a branch-free min over all M slots.
@@ -167,11 +168,9 @@ DI size_t logi(const Dev& D, const X& x, uint32_t d, uint32_t i) {
 // One node's scalar state, loaded into registers at the start of an event
 // (one batch of independent loads) and stored back at its end.
 struct NC {
-  uint32_t f, term, commit, applied, last, snap, snapt, ectr, nctr, pexp, slen, tmem;
+  uint32_t f, term, commit, applied, last, snap, snapt, ectr, nctr, pexp, slen, lastt;
 };
-// words 0..11 of the node record as three 16-B accesses. Word 11 (NF_TIMER) is
-// only read in the launch prologue and written in the epilogue (timers live in
-// registers), so writing back its stale copy in between is harmless.
+// words 0..11 of the node record as three 16-B accesses
 DI NC load_node(const Dev& D, const X& x, uint32_t d) {
   const uint4* p = reinterpret_cast<const uint4*>(NDP(d));
   const uint4 a = p[0], b = p[1], c = p[2];
@@ -181,11 +180,12 @@ DI void store_node(const Dev& D, const X& x, uint32_t d, const NC& n) {
   uint4* p = reinterpret_cast<uint4*>(NDP(d));
   p[0] = make_uint4(n.f, n.term, n.commit, n.applied);
   p[1] = make_uint4(n.last, n.snap, n.snapt, n.ectr);
-  p[2] = make_uint4(n.nctr, n.pexp, n.slen, n.tmem);
+  p[2] = make_uint4(n.nctr, n.pexp, n.slen, n.lastt);
 }
 DI uint32_t term_at(const Dev& D, const X& x, uint32_t d, const NC& n, uint32_t i) {
   if (i == 0) return 0;
   if (i == n.snap) return n.snapt;
+  if (i == n.last) return n.lastt;
   return D.log[logi(D, x, d, i)].term;
 }
 
@@ -431,8 +431,10 @@ DI void node_apply(const Dev& D, X& x, uint32_t me, NC& d, bool& kvready) {
 }
 
 // commit = the majority-th largest of the match indices mv[] (mv[me] = last),
-// if that entry is from the current term
-DI void advance_commit(const Dev& D, X& x, uint32_t me, NC& d, const uint32_t (&mv)[MR_MAX_NODES]) {
+// if that entry is from the current term: for a leader, exactly the entries
+// above its base lbase (mr_dev.h NF record note), so no log access
+DI void advance_commit(const Dev& D, X& x, uint32_t me, NC& d, const uint32_t (&mv)[MR_MAX_NODES],
+                       uint32_t lbase) {
   uint32_t maj = D.n / 2 + 1, N = 0;
 #pragma unroll
   for (uint32_t i = 0; i < MR_MAX_NODES; i++) {
@@ -441,7 +443,7 @@ DI void advance_commit(const Dev& D, X& x, uint32_t me, NC& d, const uint32_t (&
     for (uint32_t j = 0; j < MR_MAX_NODES; j++) ge += (j < D.n && mv[j] >= mv[i]) ? 1u : 0u;
     if (i < D.n && ge >= maj && mv[i] > N) N = mv[i];
   }
-  if (N > d.commit && term_at(D, x, me, d, N) == d.term) d.commit = N;
+  if (N > d.commit && N > lbase) d.commit = N;  // term_at(N) == term
 }
 
 // AppendEntries / InstallSnapshot acknowledgement up to xv; returns the peer
@@ -450,17 +452,18 @@ DI void advance_commit(const Dev& D, X& x, uint32_t me, NC& d, const uint32_t (&
 DI uint32_t on_ack(const Dev& D, X& x, uint32_t me, NC& d, uint32_t p, uint32_t xv) {
   // constant indices only: a select chain over a per-lane index is turned
   // back into a dynamically indexed scratch array by the compiler
-  uint32_t mv[MR_MAX_NODES], mp = 0;
+  uint32_t mv[MR_MAX_NODES], mp = 0, lbase = 0;
 #pragma unroll
   for (uint32_t q = 0; q < MR_MAX_NODES; q++) {
-    const uint32_t v = (q < D.n && q != me) ? PR(PF_MATCH, me, q) : 0u;
+    const uint32_t v = q < D.n ? PR(PF_MATCH, me, q) : 0u;  // match[me] = the leader base
     mp = (q == p) ? v : mp;
+    lbase = (q == me) ? v : lbase;
     mv[q] = (q == me) ? d.last : ((q == p && xv > v) ? xv : v);
   }
   uint32_t nx = PR(PF_NEXT, me, p);
   if (xv > mp) PR(PF_MATCH, me, p) = xv;
   if (xv + 1 > nx) { nx = xv + 1; PR(PF_NEXT, me, p) = nx; }
-  advance_commit(D, x, me, d, mv);
+  advance_commit(D, x, me, d, mv, lbase);
   return nx <= d.last ? (1u << p) : 0u;  // still behind: pipeline the next batch
 }
 
@@ -541,7 +544,7 @@ DI void node_event(const Dev& D, X& x, bool is_msg, uint32_t tnode, uint32_t slo
     const uint32_t role = f_role(d.f), term = d.term;
     switch (type) {
       case M_RV_REQ: {
-        uint32_t lt = term_at(D, x, me, d, d.last);
+        const uint32_t lt = d.lastt;  // term_at(last)
         bool up = (mc > lt) || (mc == lt && mb >= d.last);
         uint32_t voted = f_voted(d.f);
         bool granted = (mterm == term) && (voted == 15u || voted == ma) && up;
@@ -607,6 +610,7 @@ DI void node_event(const Dev& D, X& x, bool is_msg, uint32_t tnode, uint32_t slo
             guard_log_write(D, x, me, d.pexp, i);
             D.log[logi(D, x, me, i)] = pe[q];
             d.last = i;
+            d.lastt = pe[q].term;
             CMAX(CNT_MAX_LOG, i - d.snap);
           }
         }
@@ -637,7 +641,7 @@ DI void node_event(const Dev& D, X& x, bool is_msg, uint32_t tnode, uint32_t slo
         reset_timer(D, x, me, d);
         uint32_t idx = ma;
         if (idx > d.commit) {
-          if (!(idx <= d.last && term_at(D, x, me, d, idx) == mb)) d.last = idx;
+          if (!(idx <= d.last && term_at(D, x, me, d, idx) == mb)) { d.last = idx; d.lastt = mb; }
           d.snap = idx; d.snapt = mb; NSV(me) = MSV(slot);
           d.commit = idx; d.applied = idx;
           storage_snapshot(D, x, me, d.slen, idx);
@@ -675,25 +679,27 @@ DI void node_event(const Dev& D, X& x, bool is_msg, uint32_t tnode, uint32_t slo
     PROF(P_APPLY);
   }
   if (mode == SEND_REPLY) peers = 1u << src;
-  const uint32_t lt = mode == SEND_VOTE ? term_at(D, x, me, d, d.last) : 0u;
+  const uint32_t lt = mode == SEND_VOTE ? d.lastt : 0u;  // term_at(last)
   // appends: next[p] of every peer, then the terms at next[p] - 1, as two
   // batches of independent loads, staged in LDS for the send loop
   uint64_t snapv = 0;
-  if (mode == SEND_APPEND) {
+  if (mode == SEND_APPEND) {  // only a leader appends
     uint32_t nxa[MR_MAX_NODES];
     bool any_is = false;
+    const uint32_t lbase = PR(PF_MATCH, me, me);
 #pragma unroll
     for (uint32_t p = 0; p < MR_MAX_NODES; p++) {
       nxa[p] = bit(peers, p) ? PR(PF_NEXT, me, p) : 0u;
       any_is |= bit(peers, p) && nxa[p] <= d.snap;
     }
 #pragma unroll
-    for (uint32_t p = 0; p < MR_MAX_NODES; p++) {
+    for (uint32_t p = 0; p < MR_MAX_NODES; p++) {  // term_at(next[p] - 1)
       const uint32_t pv = nxa[p] - 1u;
-      const bool ld = bit(peers, p) && nxa[p] > d.snap && pv != 0u && pv != d.snap;
+      const bool ld = bit(peers, p) && nxa[p] > d.snap && pv != 0u && pv != d.snap &&
+                      pv != d.last && pv <= lbase;
       const uint32_t t = ld ? D.log[logi(D, x, me, pv)].term : 0u;
       LNX(p) = nxa[p];
-      LPT(p) = (pv == d.snap) ? d.snapt : t;  // term_at(pv); pv == 0 -> 0
+      LPT(p) = pv == 0u ? 0u : pv == d.snap ? d.snapt : pv == d.last ? d.lastt : pv > lbase ? d.term : t;
     }
     if (any_is) snapv = NSV(me);
   }
@@ -795,8 +801,8 @@ DI bool t_start(const Dev& D, X& x, uint32_t i, uint64_t v, uint32_t& idx, uint3
   ND(NF_PEXP, i) = pexp;
   D.log[li] = LE{term, 0u, v};
   ND(NF_LAST, i) = last;
+  ND(NF_LASTT, i) = term;
   CMAX(CNT_MAX_LOG, last - snap);
-  PR(PF_MATCH, i, i) = last;
   idx = last;
   return true;
 }
@@ -931,7 +937,7 @@ __global__ void __launch_bounds__(STEP_BLOCK, MR_WAVES_PER_EU) step_kernel(Dev D
     x.conn = CS(CS_CONN); x.alive = CS(CS_ALIVE); x.twake = CS(CS_TWAKE);
     if constexpr (nthr(S) > 0) { x.cwake = CS(CS_CWAKE); x.ctid = CS(CS_CTID); x.cslot = CS(CS_CSLOT); }
 #pragma unroll
-    for (uint32_t d = 0; d < MR_MAX_NODES; d++) x.timer[d] = d < D.n ? ND(NF_TIMER, d) : INF_T;
+    for (uint32_t d = 0; d < MR_MAX_NODES; d++) x.timer[d] = d < D.n ? TMR(d) : INF_T;
     x.free_mask = C64(C64_FREE); x.digest = C64(C64_DIGEST); x.mmin = C64(C64_MMIN);
 #if !MR_CNT_MEM
 #pragma unroll
@@ -1025,7 +1031,7 @@ __global__ void __launch_bounds__(STEP_BLOCK, MR_WAVES_PER_EU) step_kernel(Dev D
   if constexpr (nthr(S) > 0) { CS(CS_CWAKE) = x.cwake; CS(CS_CTID) = x.ctid; CS(CS_CSLOT) = x.cslot; }
 #pragma unroll
   for (uint32_t d = 0; d < MR_MAX_NODES; d++)
-    if (d < D.n) ND(NF_TIMER, d) = x.timer[d];
+    if (d < D.n) TMR(d) = x.timer[d];
   C64(C64_FREE) = x.free_mask; C64(C64_DIGEST) = x.digest; C64(C64_MMIN) = x.mmin;
 #if !MR_CNT_MEM
 #pragma unroll
@@ -1053,7 +1059,7 @@ __global__ void __launch_bounds__(256) reset_kernel(Dev D) {
   for (uint32_t d = 0; d < D.n; d++) {
     for (uint32_t f = 0; f < NF__N; f++) ND(f, d) = 0;
     ND(NF_FLAGS, d) = 15u << 4;  // follower, voted none (down, disconnected: CS_ALIVE/CS_CONN = 0)
-    ND(NF_TIMER, d) = INF_T;
+    TMR(d) = INF_T;
     ND(NF_SLEN, d) = 1;
     ND(NF_PLO, d) = 1;  // no pending payload range
     NSV(d) = 0;
