@@ -28,13 +28,21 @@ SCN_IDS = list(range(1, 30))
 N_GROUPS = 8
 
 
+# the scenarios' default server counts (mr_dev.h k_default_n): each scenario
+# gets an instance sized for it (NB = 3 or 5) and one for up to 8 servers
+DEFAULT_N = [0, 3, 3, 7, 5, 3, 5, 3, 3, 5, 3, 3, 5, 3, 5, 5, 5, 5, 5, 3, 3, 3, 3, 3, 5, 5, 5, 5, 3, 3]
+
+
 def _units(csrc):
     kern = os.path.join(csrc, "mr_kernel.hip")
-    units = [(kern, "common", ["-DMR_COMMON=1", "-DMR_SCN_LIST="])]
-    for g in range(N_GROUPS):
-        ids = SCN_IDS[g::N_GROUPS]
-        lst = " ".join(f"MR_INST({i})" for i in ids)
-        units.append((kern, f"scn{g}", ["-DMR_COMMON=0", f"-DMR_SCN_LIST={lst}"]))
+    units = [(kern, "common", ["-DMR_COMMON=1", "-DMR_SCN_LIST=", "-DMR_NB=8"])]
+    for nb in (3, 5, 8):
+        ids = [i for i in SCN_IDS if nb == 8 or DEFAULT_N[i] == nb]
+        ng = max(1, min(N_GROUPS, (len(ids) + 2) // 3))
+        for g in range(ng):
+            lst = " ".join(f"MR_INST({i})" for i in ids[g::ng])
+            units.append((kern, f"nb{nb}_{g}", ["-DMR_COMMON=0", f"-DMR_SCN_LIST={lst}",
+                                                f"-DMR_NB={nb}"]))
     for src in sorted(glob.glob(os.path.join(csrc, "*.cpp"))):
         units.append((src, os.path.splitext(os.path.basename(src))[0], []))
     return units
@@ -53,14 +61,21 @@ def build_hip(force=False, verbose=False, extra=(), out=None):
     os.makedirs(objdir, exist_ok=True)
     base = ["hipcc", f"--offload-arch={ARCH}", "-O3", "-fPIC", "-std=c++17", "-Wall",
             "-Wno-unused-function", *extra]
-    jobs, objs = [], []
+    jobs, objs, running = [], [], []
+    njobs = max(1, min(16, os.cpu_count() or 1))
     for src, name, flags in _units(csrc):
         obj = os.path.join(objdir, name + ".o")
         objs.append(obj)
         cmd = base + flags + ["-c", src, "-o", obj]
         if verbose:
             print(" ".join(cmd))
-        jobs.append((cmd, subprocess.Popen(cmd)))
+        while len(running) >= njobs:
+            running = [p for p in running if p.poll() is None]
+            if len(running) >= njobs:
+                running[0].wait()
+        p = subprocess.Popen(cmd)
+        running.append(p)
+        jobs.append((cmd, p))
     bad = [c for c, p in jobs if p.wait() != 0]
     if bad:
         raise RuntimeError("hipcc failed: " + " ".join(bad[0]))

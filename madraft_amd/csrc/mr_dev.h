@@ -154,9 +154,13 @@ constexpr uint32_t nthr(uint32_t s) {
          : s == MR_SCN_UNRELIABLE_AGREE_2C ? 64u : 0u;
 }
 
-// one step-kernel instance per scenario (mr_kernel.hip launch_step_t<S>)
-template <uint32_t S>
+// step-kernel instances (mr_kernel.hip launch_step_t<S, NB>): per scenario, one
+// sized for its default server count (nb_of) and one for up to 8 servers
+template <uint32_t S, uint32_t NB>
 hipError_t launch_step_t(const Dev& D, uint32_t budget, hipStream_t s);
+constexpr uint8_t k_default_n[] = {0, 3, 3, 7, 5, 3, 5, 3, 3, 5, 3, 3, 5, 3, 5,
+                                   5, 5, 5, 5, 3, 3, 3, 3, 3, 5, 5, 5, 5, 3, 3};
+constexpr uint32_t nb_of(uint32_t s) { return k_default_n[s] <= 5 ? k_default_n[s] : 8u; }
 #define MR_ALL_SCNS                                                                       \
   MR_INST(1) MR_INST(2) MR_INST(3) MR_INST(4) MR_INST(5) MR_INST(6) MR_INST(7) MR_INST(8) \
   MR_INST(9) MR_INST(10) MR_INST(11) MR_INST(12) MR_INST(13) MR_INST(14) MR_INST(16)      \

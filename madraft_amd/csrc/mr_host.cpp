@@ -18,8 +18,10 @@ namespace mr {
 // the step-kernel instance of scenario `scn` (instances: MR_ALL_SCNS)
 hipError_t launch_step(const Dev& D, uint32_t scn, uint32_t budget, hipStream_t s) {
   switch (scn) {
-#define MR_INST(S) \
-  case S: return launch_step_t<S>(D, budget, s);
+#define MR_INST(S)                                                                  \
+  case S:                                                                           \
+    return D.n <= nb_of(S) ? launch_step_t<S, nb_of(S)>(D, budget, s)              \
+                           : launch_step_t<S, MR_MAX_NODES>(D, budget, s);
     MR_ALL_SCNS
 #undef MR_INST
     default: return hipErrorInvalidValue;

@@ -25,7 +25,15 @@
 
 namespace mr {
 
-#define DI __device__ __forceinline__
+// internal linkage: this file is compiled several times with different MR_NB
+#define DI static __device__ __forceinline__
+// node-count bound of this translation unit's kernels: per-node register arrays
+// and unrolled node loops are sized NB (the scenario's server count, or 8), so
+// a 5-server test does not pay for 8 (memory layouts keep MR_MAX_NODES)
+#ifndef MR_NB
+#define MR_NB MR_MAX_NODES
+#endif
+constexpr uint32_t NB = MR_NB;
 constexpr uint32_t INF_T = 0xFFFFFFFFu;
 constexpr uint32_t LOSS_Q32 = 429496729u;  // floor(0.1 * 2^32), tester.rs:130
 [[maybe_unused]] constexpr uint64_t FNV_OFF = 0xCBF29CE484222325ull;
@@ -41,7 +49,7 @@ struct X {
   uint32_t cwake, ctid, cslot;      // kvraft: earliest client thread (wake, tid, slot)
   uint32_t conn, alive;  // node bit masks: connected (net clog state), started (tester.rs:24-25)
   uint64_t free_mask, digest, mmin;
-  uint32_t timer[MR_MAX_NODES];  // node timers (election / heartbeat deadline), INF_T = none
+  uint32_t timer[NB];  // node timers (election / heartbeat deadline), INF_T = none
 #if !MR_CNT_MEM
   uint32_t cnt[CNT__N];
 #endif
@@ -126,12 +134,12 @@ DI uint32_t u_range(uint32_t w, uint32_t lo, uint32_t hi) {
 DI uint32_t get_timer(const X& x, uint32_t d) {
   uint32_t v = x.timer[0];
 #pragma unroll
-  for (uint32_t j = 1; j < MR_MAX_NODES; j++) v = (d == j) ? x.timer[j] : v;
+  for (uint32_t j = 1; j < NB; j++) v = (d == j) ? x.timer[j] : v;
   return v;
 }
 DI void set_timer(X& x, uint32_t d, uint32_t t) {
 #pragma unroll
-  for (uint32_t j = 0; j < MR_MAX_NODES; j++) x.timer[j] = (d == j) ? t : x.timer[j];
+  for (uint32_t j = 0; j < NB; j++) x.timer[j] = (d == j) ? t : x.timer[j];
 }
 
 // Philox4x32-10 with counter (c0, c1, c2, 0) and key (k0, k1); returns (w0, w1).
@@ -433,14 +441,14 @@ DI void node_apply(const Dev& D, X& x, uint32_t me, NC& d, bool& kvready) {
 // commit = the majority-th largest of the match indices mv[] (mv[me] = last),
 // if that entry is from the current term: for a leader, exactly the entries
 // above its base lbase (mr_dev.h NF record note), so no log access
-DI void advance_commit(const Dev& D, X& x, uint32_t me, NC& d, const uint32_t (&mv)[MR_MAX_NODES],
+DI void advance_commit(const Dev& D, X& x, uint32_t me, NC& d, const uint32_t (&mv)[NB],
                        uint32_t lbase) {
   uint32_t maj = D.n / 2 + 1, N = 0;
 #pragma unroll
-  for (uint32_t i = 0; i < MR_MAX_NODES; i++) {
+  for (uint32_t i = 0; i < NB; i++) {
     uint32_t ge = 0;
 #pragma unroll
-    for (uint32_t j = 0; j < MR_MAX_NODES; j++) ge += (j < D.n && mv[j] >= mv[i]) ? 1u : 0u;
+    for (uint32_t j = 0; j < NB; j++) ge += (j < D.n && mv[j] >= mv[i]) ? 1u : 0u;
     if (i < D.n && ge >= maj && mv[i] > N) N = mv[i];
   }
   if (N > d.commit && N > lbase) d.commit = N;  // term_at(N) == term
@@ -452,9 +460,9 @@ DI void advance_commit(const Dev& D, X& x, uint32_t me, NC& d, const uint32_t (&
 DI uint32_t on_ack(const Dev& D, X& x, uint32_t me, NC& d, uint32_t p, uint32_t xv) {
   // constant indices only: a select chain over a per-lane index is turned
   // back into a dynamically indexed scratch array by the compiler
-  uint32_t mv[MR_MAX_NODES], mp = 0, lbase = 0;
+  uint32_t mv[NB], mp = 0, lbase = 0;
 #pragma unroll
-  for (uint32_t q = 0; q < MR_MAX_NODES; q++) {
+  for (uint32_t q = 0; q < NB; q++) {
     const uint32_t v = q < D.n ? PR(PF_MATCH, me, q) : 0u;  // match[me] = the leader base
     mp = (q == p) ? v : mp;
     lbase = (q == me) ? v : lbase;
@@ -684,16 +692,16 @@ DI void node_event(const Dev& D, X& x, bool is_msg, uint32_t tnode, uint32_t slo
   // batches of independent loads, staged in LDS for the send loop
   uint64_t snapv = 0;
   if (mode == SEND_APPEND) {  // only a leader appends
-    uint32_t nxa[MR_MAX_NODES];
+    uint32_t nxa[NB];
     bool any_is = false;
     const uint32_t lbase = PR(PF_MATCH, me, me);
 #pragma unroll
-    for (uint32_t p = 0; p < MR_MAX_NODES; p++) {
+    for (uint32_t p = 0; p < NB; p++) {
       nxa[p] = bit(peers, p) ? PR(PF_NEXT, me, p) : 0u;
       any_is |= bit(peers, p) && nxa[p] <= d.snap;
     }
 #pragma unroll
-    for (uint32_t p = 0; p < MR_MAX_NODES; p++) {  // term_at(next[p] - 1)
+    for (uint32_t p = 0; p < NB; p++) {  // term_at(next[p] - 1)
       const uint32_t pv = nxa[p] - 1u;
       const bool ld = bit(peers, p) && nxa[p] > d.snap && pv != 0u && pv != d.snap &&
                       pv != d.last && pv <= lbase;
@@ -782,7 +790,7 @@ DI void t_new(const Dev& D, X& x, bool snapshot) {  // RaftTester::new, tester.r
 DI uint32_t t_leaders(const Dev& D, X& x) {
   uint32_t m = 0;
 #pragma unroll
-  for (uint32_t i = 0; i < MR_MAX_NODES; i++)
+  for (uint32_t i = 0; i < NB; i++)
     m |= (i < D.n && f_role(ND(NF_FLAGS, i)) == R_L) ? 1u << i : 0u;
   return m;
 }
@@ -918,8 +926,9 @@ constexpr uint32_t CLS_MSG = 0, CLS_TIMER = 1, CLS_TESTER = 2, CLS_NONE = 3;
 #ifndef MR_WAVES_PER_EU
 #define MR_WAVES_PER_EU 2
 #endif
-template <uint32_t S>
+template <uint32_t S, uint32_t NBT>
 __global__ void __launch_bounds__(STEP_BLOCK, MR_WAVES_PER_EU) step_kernel(Dev D, uint32_t budget) {
+  static_assert(NBT == NB, "one node bound per translation unit");
   X x;
   x.c = blockIdx.x * blockDim.x + threadIdx.x;
 #ifdef MR_PROF
@@ -937,7 +946,7 @@ __global__ void __launch_bounds__(STEP_BLOCK, MR_WAVES_PER_EU) step_kernel(Dev D
     x.conn = CS(CS_CONN); x.alive = CS(CS_ALIVE); x.twake = CS(CS_TWAKE);
     if constexpr (nthr(S) > 0) { x.cwake = CS(CS_CWAKE); x.ctid = CS(CS_CTID); x.cslot = CS(CS_CSLOT); }
 #pragma unroll
-    for (uint32_t d = 0; d < MR_MAX_NODES; d++) x.timer[d] = d < D.n ? TMR(d) : INF_T;
+    for (uint32_t d = 0; d < NB; d++) x.timer[d] = d < D.n ? TMR(d) : INF_T;
     x.free_mask = C64(C64_FREE); x.digest = C64(C64_DIGEST); x.mmin = C64(C64_MMIN);
 #if !MR_CNT_MEM
 #pragma unroll
@@ -964,7 +973,7 @@ __global__ void __launch_bounds__(STEP_BLOCK, MR_WAVES_PER_EU) step_kernel(Dev D
         if (tcli) key = kc;
       }
 #pragma unroll
-      for (uint32_t d = 0; d < MR_MAX_NODES; d++) {  // timers of absent nodes are INF_T
+      for (uint32_t d = 0; d < NB; d++) {  // timers of absent nodes are INF_T
         uint64_t kt = ((uint64_t)x.timer[d] << 32) | (1ull << 30) | d;
         if (kt < key) { key = kt; cls = CLS_TIMER; node = d; }
       }
@@ -1030,7 +1039,7 @@ __global__ void __launch_bounds__(STEP_BLOCK, MR_WAVES_PER_EU) step_kernel(Dev D
   CS(CS_CONN) = x.conn; CS(CS_ALIVE) = x.alive; CS(CS_TWAKE) = x.twake;
   if constexpr (nthr(S) > 0) { CS(CS_CWAKE) = x.cwake; CS(CS_CTID) = x.ctid; CS(CS_CSLOT) = x.cslot; }
 #pragma unroll
-  for (uint32_t d = 0; d < MR_MAX_NODES; d++)
+  for (uint32_t d = 0; d < NB; d++)
     if (d < D.n) TMR(d) = x.timer[d];
   C64(C64_FREE) = x.free_mask; C64(C64_DIGEST) = x.digest; C64(C64_MMIN) = x.mmin;
 #if !MR_CNT_MEM
@@ -1130,12 +1139,12 @@ hipError_t launch_reduce(const Dev& D, unsigned long long* out, uint64_t cluster
 }
 #endif  // MR_COMMON
 
-template <uint32_t S>
+template <uint32_t S, uint32_t NBT>
 hipError_t launch_step_t(const Dev& D, uint32_t budget, hipStream_t s) {
   dim3 blk(STEP_BLOCK), grd((D.C + STEP_BLOCK - 1) / STEP_BLOCK);
   const size_t lds = (size_t)D.M * STEP_BLOCK * sizeof(uint64_t) +  // message keys
                     2 * MR_MAX_NODES * STEP_BLOCK * sizeof(uint32_t);  // send-loop staging
-  hipLaunchKernelGGL(step_kernel<S>, grd, blk, lds, s, D, budget);
+  hipLaunchKernelGGL((step_kernel<S, NBT>), grd, blk, lds, s, D, budget);
   return hipGetLastError();
 }
 // Step-kernel instances built by this translation unit: build.py compiles
@@ -1144,7 +1153,7 @@ hipError_t launch_step_t(const Dev& D, uint32_t budget, hipStream_t s) {
 #ifndef MR_SCN_LIST
 #define MR_SCN_LIST MR_ALL_SCNS
 #endif
-#define MR_INST(S) template hipError_t launch_step_t<S>(const Dev&, uint32_t, hipStream_t);
+#define MR_INST(S) template hipError_t launch_step_t<S, MR_NB>(const Dev&, uint32_t, hipStream_t);
 MR_SCN_LIST
 #undef MR_INST
 
