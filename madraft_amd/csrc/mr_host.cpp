@@ -73,7 +73,7 @@ struct mr_batch {
   uint32_t* h_remaining = nullptr;
   hipStream_t stream = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
-  uint32_t budget = 2048;
+  uint32_t budget = 16384;  // events per cluster per launch (MR_STEP_BUDGET)
 };
 
 extern "C" {
@@ -277,7 +277,7 @@ int mr_batch_create(const mr_cfg* cfg, mr_batch** out) {
     return set_err("hipMemset failed");
   }
   if (const char* s = std::getenv("MR_STEP_BUDGET")) b->budget = (uint32_t)std::atoi(s);
-  if (b->budget == 0) b->budget = 2048;
+  if (b->budget == 0) b->budget = 16384;
   if (mr_batch_reset(b, cfg->seed_base) != 0) {
     std::string msg = g_err;
     mr_batch_destroy(b);
