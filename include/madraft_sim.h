@@ -82,6 +82,11 @@ enum mr_scenario {
 #define MR_F_UNRELIABLE 0x1u /* set_unreliable(true) right after RaftTester::new (C2) */
 #define MR_F_NULL_RAFT 0x2u  /* skeleton node: never campaigns (as-shipped raft.rs) */
 #define MR_F_TRACE 0x4u      /* capture per-event trace for the first trace_clusters */
+#define MR_F_SAFETY 0x8u     /* Raft invariant checks at every election (SEMANTICS §11) */
+/* Known-buggy Raft variants (SEMANTICS §11), so the checkers can be shown to catch bugs the
+ * way the reference tester grades a student's raft.rs */
+#define MR_F_BUG_VOTE_TWICE 0x10u /* voters ignore votedFor: two leaders per term possible */
+#define MR_F_BUG_VOTE_STALE 0x20u /* voters skip the up-to-date check (Raft §5.4.1) */
 
 /* ---- verdicts: one code per tester panic site ---- */
 enum mr_fail {
@@ -127,6 +132,9 @@ enum mr_fail {
   MR_FAIL_CTRL_MINIMAL_LEAVE = 39,/* shard_ctrler/tests.rs:154,269 "non-minimal transfer after Leave()s" */
   MR_FAIL_CTRL_NO_LEADER = 40,    /* shard_ctrler/tests.rs:282,289 "Leader not found" */
   MR_FAIL_CTRL_SAME_CONFIG = 41,  /* shard_ctrler/tests.rs:294 assert_eq!(c, c1) */
+  /* Raft invariants (MR_F_SAFETY; Raft paper Fig. 3), not reference panic sites */
+  MR_FAIL_SAFETY_ELECTION = 42,   /* two leaders elected in one term */
+  MR_FAIL_SAFETY_COMPLETENESS = 43, /* a new leader lacks a committed (applied) entry */
   /* simulator limits (not reference panics): a cluster that hits one is reported, never passed */
   MR_FAIL_SIM_CAPACITY = 60,      /* a log / apply / sequence capacity of the config was exceeded */
   MR_FAIL_SIM_EVENT_LIMIT = 61,   /* cfg.max_events processed without a verdict */

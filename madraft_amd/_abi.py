@@ -15,6 +15,9 @@ MR_PASS = 0
 MR_F_UNRELIABLE = 0x1
 MR_F_NULL_RAFT = 0x2
 MR_F_TRACE = 0x4
+MR_F_SAFETY = 0x8
+MR_F_BUG_VOTE_TWICE = 0x10
+MR_F_BUG_VOTE_STALE = 0x20
 
 README_SEED = 1629626496  # /root/reference/README.md:48
 
@@ -47,7 +50,7 @@ FAIL_NAMES = {
     29: "KV_APPEND_BAD", 30: "CTRL_NGROUPS", 31: "CTRL_MISSING", 32: "CTRL_INVALID",
     33: "CTRL_IMBALANCED", 34: "CTRL_SERVERS", 35: "CTRL_HISTORY", 36: "CTRL_MOVE_NUM",
     37: "CTRL_MOVE_WRONG", 38: "CTRL_MINIMAL_JOIN", 39: "CTRL_MINIMAL_LEAVE", 40: "CTRL_NO_LEADER",
-    41: "CTRL_SAME_CONFIG", 60: "SIM_CAPACITY",
+    41: "CTRL_SAME_CONFIG", 42: "SAFETY_ELECTION", 43: "SAFETY_COMPLETENESS", 60: "SIM_CAPACITY",
     61: "SIM_EVENT_LIMIT", 62: "SIM_BAD_PROGRAM", 0xFFFF: "RUNNING",
 }
 

@@ -47,6 +47,8 @@ enum : uint32_t {
   CS_KVDONE = CS_CNT + CNT__N, CS_MJOIN, CS_CWAKE, CS_CTID, CS_CSLOT,  // tester threads (SEMANTICS §8-9)
   CS_NLIVE,  // live spawned threads
   CS_NOPS,   // shard_ctrler: clerk operations so far
+  CS_LRING,  // MR_F_SAFETY: (term << 4) | leader + 1 by term mod 32
+  CS_LRING_END = CS_LRING + 32,
   CS__N
 };
 // cs64 [C64__N][C]: per-cluster u64 scalars
@@ -116,7 +118,7 @@ struct alignas(16) SE {
 struct Dev {
   // config
   uint32_t C, n, log_cap, apply_cap, M, K, hb, elo, ehi, max_events;
-  uint32_t null_raft, unrel_flag, trace_clusters, trace_cap, scenario, iters;
+  uint32_t null_raft, unrel_flag, trace_clusters, trace_cap, scenario, iters, safety, bugs;
   uint64_t seed0;  // seed of cluster 0 = seed_base + cluster_base
   uint32_t* cs32;
   uint64_t* cs64;

@@ -133,6 +133,8 @@ const char* mr_fail_message(uint32_t code) {
     case MR_FAIL_CTRL_MINIMAL_LEAVE: return "non-minimal transfer after Leave()s";
     case MR_FAIL_CTRL_NO_LEADER: return "Leader not found";
     case MR_FAIL_CTRL_SAME_CONFIG: return "config differs after leader shutdown";
+    case MR_FAIL_SAFETY_ELECTION: return "election safety: two leaders in one term";
+    case MR_FAIL_SAFETY_COMPLETENESS: return "leader completeness: new leader lacks a committed entry";
     case MR_FAIL_SIM_CAPACITY: return "simulator capacity exceeded";
     case MR_FAIL_SIM_EVENT_LIMIT: return "simulator event limit exceeded";
     case MR_FAIL_SIM_BAD_PROGRAM: return "scenario program error";
@@ -203,6 +205,8 @@ int mr_batch_create(const mr_cfg* cfg, mr_batch** out) {
   D.ehi = cfg->elect_hi_us; D.max_events = cfg->max_events;
   D.null_raft = (cfg->flags & MR_F_NULL_RAFT) ? 1u : 0u;
   D.unrel_flag = (cfg->flags & MR_F_UNRELIABLE) ? 1u : 0u;
+  D.safety = (cfg->flags & MR_F_SAFETY) ? 1u : 0u;
+  D.bugs = cfg->flags & (MR_F_BUG_VOTE_TWICE | MR_F_BUG_VOTE_STALE);
   D.trace_clusters = (cfg->flags & MR_F_TRACE) ? cfg->trace_clusters : 0u;
   D.trace_cap = cfg->trace_cap;
   D.scenario = scn;

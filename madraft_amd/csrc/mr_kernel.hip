@@ -110,10 +110,12 @@ __shared__ unsigned long long s_prof[STEP_BLOCK / 64][2 * P__N + 1];
 #define MR_CNT_MEM 0
 #endif
 #if MR_CNT_MEM
+#define CNT_GET(k) CS(CS_CNT + (k))
 #define CADD(k, v) __hip_atomic_fetch_add(&CS(CS_CNT + (k)), (uint32_t)(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
 #define CMAX(k, v) __hip_atomic_fetch_max(&CS(CS_CNT + (k)), (uint32_t)(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
 #else
 #define CADD(k, v) (x.cnt[k] += (v))
+#define CNT_GET(k) x.cnt[k]
 #define CMAX(k, v) do { uint32_t v_ = (v); if (v_ > x.cnt[k]) x.cnt[k] = v_; } while (0)
 #endif
 // node flag word: role[0:2) voted[4:8) (15 = none) inc[8:16) votes[16:24)
@@ -454,6 +456,17 @@ DI void advance_commit(const Dev& D, X& x, uint32_t me, NC& d, const uint32_t (&
   if (N > d.commit && N > lbase) d.commit = N;  // term_at(N) == term
 }
 
+// MR_F_SAFETY (SEMANTICS §11): election safety over a ring of the last 32
+// terms' leaders; leader completeness for the highest index any server applied
+DI void safety_on_leader(const Dev& D, X& x, uint32_t me, const NC& d) {
+  const uint32_t t = d.term, e = CS(CS_LRING + (t & 31u));
+  if ((e >> 4) == t && (e & 15u) != me + 1u) { fail(D, x, MR_FAIL_SAFETY_ELECTION); return; }
+  CS(CS_LRING + (t & 31u)) = (t << 4) | (me + 1u);
+  const uint32_t j = CNT_GET(CNT_MAX_INDEX);
+  if (j > d.snap && (j > d.last || D.log[logi(D, x, me, j)].val != D.stor[(size_t)x.c * D.apply_cap + j].val))
+    fail(D, x, MR_FAIL_SAFETY_COMPLETENESS);
+}
+
 // AppendEntries / InstallSnapshot acknowledgement up to xv; returns the peer
 // mask to send a follow-up append to. The match indices of every peer and
 // next[p] are loaded as one batch of independent loads.
@@ -555,7 +568,9 @@ DI void node_event(const Dev& D, X& x, bool is_msg, uint32_t tnode, uint32_t slo
         const uint32_t lt = d.lastt;  // term_at(last)
         bool up = (mc > lt) || (mc == lt && mb >= d.last);
         uint32_t voted = f_voted(d.f);
-        bool granted = (mterm == term) && (voted == 15u || voted == ma) && up;
+        if (D.bugs & MR_F_BUG_VOTE_STALE) up = true;
+        const bool free_vote = voted == 15u || voted == ma || (D.bugs & MR_F_BUG_VOTE_TWICE);
+        bool granted = (mterm == term) && free_vote && up;
         if (granted) {
           d.f = f_set(d.f, 4, 4, ma);
           reset_timer(D, x, me, d);
@@ -568,6 +583,10 @@ DI void node_event(const Dev& D, X& x, bool is_msg, uint32_t tnode, uint32_t slo
           uint32_t votes = f_votes(d.f) | (1u << src);
           d.f = f_set(d.f, 16, 8, votes);
           if ((uint32_t)__builtin_popcount(votes) > D.n / 2) {  // become leader
+            if (D.safety) {
+              safety_on_leader(D, x, me, d);
+              if (x.code != RUN) return;
+            }
             d.f = f_set(d.f, 0, 2, R_L);
             CADD(CNT_LEADERS, 1u);
             for (uint32_t p = 0; p < D.n; p++) {

@@ -67,7 +67,7 @@ def fail_message(code):
 
 def make_cfg(test, clusters=1, seed=_abi.README_SEED, *, nodes=None, iters=0, unreliable=False,
              null_raft=False, trace_clusters=0, trace_cap=None, cluster_base=0, device=0,
-             **overrides):
+             safety=False, **overrides):
     """mr_cfg for `test` with the reference's defaults (mr_cfg_init) plus overrides."""
     scn = _abi.SCENARIO_ID.get(test)
     if scn is None:
@@ -87,11 +87,14 @@ def make_cfg(test, clusters=1, seed=_abi.README_SEED, *, nodes=None, iters=0, un
         cfg.flags |= _abi.MR_F_UNRELIABLE
     if null_raft:
         cfg.flags |= _abi.MR_F_NULL_RAFT
+    if safety:
+        cfg.flags |= _abi.MR_F_SAFETY
     if trace_clusters:
         cfg.flags |= _abi.MR_F_TRACE
         cfg.trace_clusters = int(trace_clusters)
         if trace_cap:
             cfg.trace_cap = int(trace_cap)
+    cfg.flags |= int(overrides.pop("flags", 0))  # extra MR_F_* bits (SAFETY, BUG_*)
     for k, v in overrides.items():
         setattr(cfg, k, int(v))
     return cfg

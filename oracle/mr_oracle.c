@@ -124,6 +124,7 @@ typedef struct {
   OClerk ck[CK_SLOTS]; OThr th[MAX_THR];
   uint64_t* cval; uint32_t* cidx; /* churn values [3][CHURN_VCAP] + their indices */
   uint32_t ctrl_mode, nops, ncfg[MR_MAX_NODES];
+  uint32_t lring[32]; /* MR_F_SAFETY: (term << 4) | leader + 1 by term mod 32 */
   OCfg* cfgs; /* [MR_MAX_NODES][CFG_CAP] */
   OOp* ops;   /* [OP_CAP] */
   uint32_t churn_stop;
@@ -456,8 +457,21 @@ static void send_append(OSim* s, uint32_t me, uint32_t p) {
   net_send(s, me, p, &m);
 }
 
+/* MR_F_SAFETY (SEMANTICS §11): election safety over a ring of the last 32 terms'
+ * leaders, and leader completeness for the highest index any server applied */
+static void safety_on_leader(OSim* s, uint32_t me) {
+  ONode* d = &s->nd[me];
+  uint32_t t = d->term, e = s->lring[t & 31u];
+  if ((e >> 4) == t && (e & 15u) != me + 1) t_fail(s, MR_FAIL_SAFETY_ELECTION);
+  s->lring[t & 31u] = (t << 4) | (me + 1);
+  uint32_t j = (uint32_t)s->r.max_index;
+  if (j > d->snap_idx && (j > d->last || d->lval[lpos(s, j)] != s->sval[j]))
+    t_fail(s, MR_FAIL_SAFETY_COMPLETENESS);
+}
+
 static void become_leader(OSim* s, uint32_t me) {
   ONode* d = &s->nd[me];
+  if (s->cfg.flags & MR_F_SAFETY) safety_on_leader(s, me);
   d->role = R_L;
   s->r.leaders_elected++;
   for (uint32_t p = 0; p < s->n; p++) { d->next[p] = d->last + 1; d->match[p] = 0; }
@@ -574,7 +588,9 @@ static void deliver(OSim* s, OMsg* m) {
     case M_RV_REQ: {
       uint32_t lt = term_at(s, d, d->last);
       int up = (m->c > lt) || (m->c == lt && m->b >= d->last);
-      int granted = (m->term == d->term) && (d->voted < 0 || d->voted == (int32_t)m->a) && up;
+      if (s->cfg.flags & MR_F_BUG_VOTE_STALE) up = 1;
+      int free_vote = (d->voted < 0 || d->voted == (int32_t)m->a) || (s->cfg.flags & MR_F_BUG_VOTE_TWICE);
+      int granted = (m->term == d->term) && free_vote && up;
       if (granted) { d->voted = (int32_t)m->a; reset_timer(s, me); }
       reply(s, me, m, M_RV_REP, (uint32_t)granted, 0);
     } break;
@@ -1894,6 +1910,7 @@ static void sim_reset(OSim* s, uint64_t cluster) {
   memset(s->kv_dedup, 0, sizeof s->kv_dedup); memset(s->pend, 0, sizeof s->pend);
   memset(s->ck, 0, sizeof s->ck); memset(s->th, 0, sizeof s->th); s->churn_stop = 0;
   s->ctrl_mode = 0; s->nops = 0;
+  memset(s->lring, 0, sizeof s->lring);
   for (uint32_t i = 0; i < MR_MAX_NODES; i++) { /* the initial config, num 0 */
     s->ncfg[i] = 1;
     memset(&s->cfgs[i * CFG_CAP], 0, sizeof(OCfg));
@@ -2023,6 +2040,8 @@ const char* mro_fail_message(uint32_t code) {
     case MR_FAIL_KV_GET_WRONG: return "get wrong value";
     case MR_FAIL_KV_MISSING: return "missing element in Append result";
     case MR_FAIL_KV_APPEND_BAD: return "duplicate or wrong order element in Append result";
+    case MR_FAIL_SAFETY_ELECTION: return "election safety: two leaders in one term";
+    case MR_FAIL_SAFETY_COMPLETENESS: return "leader completeness: new leader lacks a committed entry";
     case MR_FAIL_SIM_CAPACITY: return "simulator capacity exceeded";
     case MR_FAIL_SIM_EVENT_LIMIT: return "simulator event limit exceeded";
     default: return "scenario assertion failed";

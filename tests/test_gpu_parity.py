@@ -132,3 +132,19 @@ def test_baseline_sizes(hip, oracle, test, clusters, kw):
     for k in rng.choice(clusters, 48, replace=False):
         oc, ot, od, _ = oracle.run_batch(cfg, int(k), 1)
         assert (oc[0], ot[0], od[0]) == (code[k], t[k], dig[k]), (test, int(k))
+
+
+@pytest.mark.parametrize("test,flags", [
+    ("figure_8_unreliable_2c", _abi.MR_F_SAFETY),
+    ("unreliable_3a", _abi.MR_F_SAFETY),
+    ("many_election_2a", _abi.MR_F_SAFETY | _abi.MR_F_BUG_VOTE_TWICE),
+    ("figure_8_2c", _abi.MR_F_SAFETY | _abi.MR_F_BUG_VOTE_STALE),
+])
+def test_safety_checks_bit_exact(hip, oracle, test, flags):
+    """MR_F_SAFETY checks (and the buggy-Raft variants they catch) on the GPU:
+    same verdicts, times and traces as the oracle."""
+    code, _ = compare(hip, oracle, test, 512, flags=flags)
+    if flags & (_abi.MR_F_BUG_VOTE_TWICE | _abi.MR_F_BUG_VOTE_STALE):
+        assert np.isin(code, [42, 43]).sum() >= 10
+    else:
+        assert not np.isin(code, [42, 43]).any()

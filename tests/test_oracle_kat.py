@@ -119,3 +119,33 @@ def test_golden_fixtures(oracle):
         assert t.tolist() == case["time_us"], case["test"]
         assert [format(int(d), "016x") for d in dig] == case["digest"], case["test"]
         assert s["events"] == case["events"], case["test"]
+
+
+@pytest.mark.parametrize("test", ["figure_8_unreliable_2c", "figure_8_2c", "unreliable_churn_2c",
+                                  "persist3_2c", "snapshot_install_unreliable_crash_2d", "fail_agree_2b",
+                                  "unreliable_3a", "multi_4a"])
+def test_safety_invariants_hold(oracle, test):
+    """MR_F_SAFETY (docs/SEMANTICS.md §11): election safety and leader completeness
+    hold at every election, and the checks observe without changing the run."""
+    base = oracle.cfg(test)
+    code0, t0, dig0, s0 = oracle.run_batch(base, 0, 48)
+    cfg = oracle.cfg(test, flags=_abi.MR_F_SAFETY)
+    code, t, dig, s = oracle.run_batch(cfg, 0, 48)
+    assert (code == code0).all() and (t == t0).all() and (dig == dig0).all()
+    assert not np.isin(code, [42, 43]).any()
+    assert s["events"] == s0["events"] and s["leaders_elected"] > 0
+
+
+@pytest.mark.parametrize("bug,test,code_", [
+    (_abi.MR_F_BUG_VOTE_TWICE, "many_election_2a", 42),
+    (_abi.MR_F_BUG_VOTE_TWICE, "figure_8_unreliable_2c", 42),
+    (_abi.MR_F_BUG_VOTE_STALE, "figure_8_2c", 43),
+    (_abi.MR_F_BUG_VOTE_STALE, "persist3_2c", 43),
+])
+def test_safety_catches_buggy_raft(oracle, bug, test, code_):
+    """A Raft with a known voting bug is caught: with MR_F_SAFETY by the invariant
+    checker, without it (on most seeds) by the reference tester's own checks."""
+    code, *_ = oracle.run_batch(oracle.cfg(test, flags=bug | _abi.MR_F_SAFETY), 0, 200)
+    assert (code == code_).sum() >= 10
+    plain, *_ = oracle.run_batch(oracle.cfg(test, flags=bug), 0, 200)
+    assert (plain != 0).sum() >= 9
