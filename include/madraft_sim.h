@@ -75,8 +75,28 @@ enum mr_scenario {
   /* shard_ctrler (src/shard_ctrler/tests.rs) over 3 servers */
   MR_SCN_CTRL_BASIC_4A = 28,             /* shard_ctrler/tests.rs:24-166  */
   MR_SCN_CTRL_MULTI_4A = 29,             /* shard_ctrler/tests.rs:168-299 */
+  /* kvraft generic_test with partitions / restarts (src/kvraft/tests.rs:344-385) */
+  MR_SCN_KV_MANY_PARTITIONS_ONE_CLIENT_3A = 30,    /* kvraft/tests.rs:344-348 */
+  MR_SCN_KV_MANY_PARTITIONS_MANY_CLIENTS_3A = 31,  /* kvraft/tests.rs:350-354 */
+  MR_SCN_KV_PERSIST_ONE_CLIENT_3A = 32,            /* kvraft/tests.rs:356-360 */
+  MR_SCN_KV_PERSIST_CONCURRENT_3A = 33,            /* kvraft/tests.rs:362-366 */
+  MR_SCN_KV_PERSIST_CONCURRENT_UNRELIABLE_3A = 34, /* kvraft/tests.rs:368-372 */
+  MR_SCN_KV_PERSIST_PARTITION_3A = 35,             /* kvraft/tests.rs:374-378 */
+  MR_SCN_KV_PERSIST_PARTITION_UNRELIABLE_3A = 36,  /* kvraft/tests.rs:380-384 */
   MR_SCN_COUNT_
 };
+
+/* kvraft scenarios (generic_test and its variants) */
+static inline int mr_scn_is_kv(uint32_t s) {
+  return (s >= MR_SCN_KV_BASIC_3A && s <= MR_SCN_KV_UNRELIABLE_3A) ||
+         (s >= MR_SCN_KV_MANY_PARTITIONS_ONE_CLIENT_3A && s <= MR_SCN_KV_PERSIST_PARTITION_UNRELIABLE_3A);
+}
+/* default log / apply capacity of a kvraft scenario (no snapshots: every op stays in the log) */
+static inline uint32_t mr_kv_log_cap(uint32_t s) {
+  return (s == MR_SCN_KV_BASIC_3A || s == MR_SCN_KV_UNRELIABLE_3A ||
+          s == MR_SCN_KV_PERSIST_CONCURRENT_UNRELIABLE_3A || s == MR_SCN_KV_PERSIST_PARTITION_UNRELIABLE_3A ||
+          s == MR_SCN_KV_MANY_PARTITIONS_ONE_CLIENT_3A || s == MR_SCN_KV_PERSIST_ONE_CLIENT_3A) ? 2048u : 8192u;
+}
 
 /* ---- flags ---- */
 #define MR_F_UNRELIABLE 0x1u /* set_unreliable(true) right after RaftTester::new (C2) */

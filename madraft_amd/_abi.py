@@ -31,12 +31,18 @@ SCENARIOS = [
     "snapshot_install_unreliable_2d", "snapshot_install_crash_2d",
     "snapshot_install_unreliable_crash_2d", "figure_8_unreliable_crash", "basic_3a",
     "concurrent_3a", "unreliable_3a", "basic_4a", "multi_4a",
+    "many_partitions_one_client_3a", "many_partitions_many_clients_3a", "persist_one_client_3a",
+    "persist_concurrent_3a", "persist_concurrent_unreliable_3a", "persist_partition_3a",
+    "persist_partition_unreliable_3a",
 ]
 SCENARIO_ID = {n: i for i, n in enumerate(SCENARIOS) if n}
 # tests that still need multi-threaded tester programs (spawn_local); not built yet
 UNSUPPORTED = set()
 # kvraft generic_test (src/kvraft/tests.rs:65-238), BASELINE config 5
-KV_TESTS = ["basic_3a", "concurrent_3a", "unreliable_3a"]
+KV_TESTS = ["basic_3a", "concurrent_3a", "unreliable_3a", "many_partitions_one_client_3a",
+            "many_partitions_many_clients_3a", "persist_one_client_3a", "persist_concurrent_3a",
+            "persist_concurrent_unreliable_3a", "persist_partition_3a",
+            "persist_partition_unreliable_3a"]
 GPU_UNSUPPORTED = set()
 
 FAIL_NAMES = {

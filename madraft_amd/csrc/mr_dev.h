@@ -49,6 +49,8 @@ enum : uint32_t {
   CS_NOPS,   // shard_ctrler: clerk operations so far
   CS_LRING,  // MR_F_SAFETY: (term << 4) | leader + 1 by term mod 32
   CS_LRING_END = CS_LRING + 32,
+  CS_CUT,    // server links cut (disconnect2): bit 8 (i mod 4) + j of word CS_CUT + i / 4
+  CS_CUT_END = CS_CUT + 2,
   CS__N
 };
 // cs64 [C64__N][C]: per-cluster u64 scalars
@@ -81,14 +83,16 @@ struct alignas(16) LE {
 enum : uint32_t { KV_GET = 0, KV_PUT = 1, KV_APPEND = 2 };
 enum : uint32_t { KV_OK = 0, KV_WRONG_LEADER = 1, KV_FAILED = 2 };
 constexpr uint32_t CLERK_HOST = 8;  // clerk c is host 8 + c
-constexpr uint32_t KV_SLOTS = 6;    // tester thread / clerk slots: 0 = test body + ck, 1 + cli
+constexpr uint32_t KV_SLOTS = 7;    // tester thread / clerk slots: 0 = test body + ck, 1 + cli, partitioner
 constexpr uint32_t KV_PEND = 8;     // pending requests per server
 // kt32 [KT__N][nthr(S)][C]: a spawned tester thread (+ its clerk, kvraft) per slot.
 // Words KT_W.. are the thread's own frame: kvraft clerk fields, churn client
 // (x lo/hi, index, timeout step, values), or a one() task (helper frame h[0..4], cmd).
 enum : uint32_t {
   KT_TID, KT_LIVE, KT_PC, KT_J, KT_CLI, KT_TCTR, KT_WAKE, KT_ID, KT_LH, KT_SEQ, KT_TAG, KT_NCTR,
-  KT_WAITING, KT_GOT, KT_RSTAT, KT_RHINT, KT_RVAL, KT_OP, KT_KEY, KT_ELEM, KT__N
+  KT_WAITING, KT_GOT, KT_RSTAT, KT_RHINT, KT_RVAL, KT_OP, KT_KEY, KT_ELEM,
+  KT_KIND,  // 1 = generic_test partitioner (KT_PERM: its shuffled `all`, 4 bits per server)
+  KT_PERM, KT__N
 };
 constexpr uint32_t KT_W = KT_ID;
 constexpr uint32_t JOIN_ALL = 0xFFFFFFFEu;
@@ -118,7 +122,7 @@ struct alignas(16) SE {
 struct Dev {
   // config
   uint32_t C, n, log_cap, apply_cap, M, K, hb, elo, ehi, max_events;
-  uint32_t null_raft, unrel_flag, trace_clusters, trace_cap, scenario, iters, safety, bugs;
+  uint32_t null_raft, unrel_flag, trace_clusters, trace_cap, scenario, iters, safety, bugs, links;
   uint64_t seed0;  // seed of cluster 0 = seed_base + cluster_base
   uint32_t* cs32;
   uint64_t* cs64;
@@ -142,7 +146,27 @@ struct Dev {
 };
 constexpr uint32_t PROF_SLOTS = 64;
 
-constexpr bool is_kv(uint32_t s) { return s >= MR_SCN_KV_BASIC_3A && s <= MR_SCN_KV_UNRELIABLE_3A; }
+constexpr bool is_kv(uint32_t s) {
+  return (s >= MR_SCN_KV_BASIC_3A && s <= MR_SCN_KV_UNRELIABLE_3A) ||
+         (s >= MR_SCN_KV_MANY_PARTITIONS_ONE_CLIENT_3A && s <= MR_SCN_KV_PERSIST_PARTITION_UNRELIABLE_3A);
+}
+// generic_test(nclients, unreliable, crash, partitions) of a kvraft scenario (kvraft/tests.rs:222-384)
+struct KvGen { uint32_t nc; bool unrel, crash, part; };
+constexpr KvGen kv_gen(uint32_t s) {
+  switch (s) {
+    case MR_SCN_KV_BASIC_3A: return {1, false, false, false};
+    case MR_SCN_KV_CONCURRENT_3A: return {5, false, false, false};
+    case MR_SCN_KV_UNRELIABLE_3A: return {5, true, false, false};
+    case MR_SCN_KV_MANY_PARTITIONS_ONE_CLIENT_3A: return {1, false, false, true};
+    case MR_SCN_KV_MANY_PARTITIONS_MANY_CLIENTS_3A: return {5, false, false, true};
+    case MR_SCN_KV_PERSIST_ONE_CLIENT_3A: return {1, false, true, false};
+    case MR_SCN_KV_PERSIST_CONCURRENT_3A: return {5, false, true, false};
+    case MR_SCN_KV_PERSIST_CONCURRENT_UNRELIABLE_3A: return {5, true, true, false};
+    case MR_SCN_KV_PERSIST_PARTITION_3A: return {5, false, true, true};
+    case MR_SCN_KV_PERSIST_PARTITION_UNRELIABLE_3A: return {5, true, true, true};
+    default: return {0, false, false, false};
+  }
+}
 constexpr bool is_ctrl(uint32_t s) { return s == MR_SCN_CTRL_BASIC_4A || s == MR_SCN_CTRL_MULTI_4A; }
 // scenarios served by the clerk / server request path (kvraft + shard_ctrler)
 constexpr bool is_svc(uint32_t s) { return is_kv(s) || is_ctrl(s); }
@@ -161,12 +185,14 @@ constexpr uint32_t nthr(uint32_t s) {
 template <uint32_t S, uint32_t NB>
 hipError_t launch_step_t(const Dev& D, uint32_t budget, hipStream_t s);
 constexpr uint8_t k_default_n[] = {0, 3, 3, 7, 5, 3, 5, 3, 3, 5, 3, 3, 5, 3, 5,
-                                   5, 5, 5, 5, 3, 3, 3, 3, 3, 5, 5, 5, 5, 3, 3};
+                                   5, 5, 5, 5, 3, 3, 3, 3, 3, 5, 5, 5, 5, 3, 3,
+                                   5, 5, 5, 5, 5, 5, 5};
 constexpr uint32_t nb_of(uint32_t s) { return k_default_n[s] <= 5 ? k_default_n[s] : 8u; }
 #define MR_ALL_SCNS                                                                       \
   MR_INST(1) MR_INST(2) MR_INST(3) MR_INST(4) MR_INST(5) MR_INST(6) MR_INST(7) MR_INST(8) \
   MR_INST(9) MR_INST(10) MR_INST(11) MR_INST(12) MR_INST(13) MR_INST(14) MR_INST(16)      \
   MR_INST(19) MR_INST(20) MR_INST(21) MR_INST(22) MR_INST(23) MR_INST(24) MR_INST(25)     \
-  MR_INST(26) MR_INST(27) MR_INST(15) MR_INST(17) MR_INST(18) MR_INST(28) MR_INST(29)
+  MR_INST(26) MR_INST(27) MR_INST(15) MR_INST(17) MR_INST(18) MR_INST(28) MR_INST(29)     \
+  MR_INST(30) MR_INST(31) MR_INST(32) MR_INST(33) MR_INST(34) MR_INST(35) MR_INST(36)
 
 }  // namespace mr

@@ -56,10 +56,14 @@ const char* k_names[MR_SCN_COUNT_] = {
     "unreliable_churn_2c", "snapshot_basic_2d", "snapshot_install_2d",
     "snapshot_install_unreliable_2d", "snapshot_install_crash_2d",
     "snapshot_install_unreliable_crash_2d", "figure_8_unreliable_crash", "basic_3a",
-    "concurrent_3a", "unreliable_3a", "basic_4a", "multi_4a"};
+    "concurrent_3a", "unreliable_3a", "basic_4a", "multi_4a",
+    "many_partitions_one_client_3a", "many_partitions_many_clients_3a", "persist_one_client_3a",
+    "persist_concurrent_3a", "persist_concurrent_unreliable_3a", "persist_partition_3a",
+    "persist_partition_unreliable_3a"};
 // servers per test (tests.rs `let servers = ..`)
 const uint8_t k_nodes[MR_SCN_COUNT_] = {0, 3, 3, 7, 5, 3, 5, 3, 3, 5, 3, 3, 5, 3,
-                                        5, 5, 5, 5, 5, 3, 3, 3, 3, 3, 5, 5, 5, 5, 3, 3};
+                                        5, 5, 5, 5, 5, 3, 3, 3, 3, 3, 5, 5, 5, 5, 3, 3,
+                                        5, 5, 5, 5, 5, 5, 5};
 
 constexpr size_t RED_N = CNT__N + 8 + 64;  // reduce_kernel output slots
 }  // namespace
@@ -156,9 +160,9 @@ int mr_cfg_init(mr_cfg* c, uint32_t scn) {
   int fig8 = scn == MR_SCN_FIGURE_8_2C || scn == MR_SCN_FIGURE_8_UNRELIABLE_2C ||
              scn == MR_SCN_FIGURE_8_UNRELIABLE_CRASH;
   int snap = scn >= MR_SCN_SNAPSHOT_BASIC_2D && scn <= MR_SCN_SNAPSHOT_INSTALL_UNRELIABLE_CRASH_2D;
-  int kv = scn >= MR_SCN_KV_BASIC_3A && scn <= MR_SCN_KV_UNRELIABLE_3A;
+  int kv = mr_scn_is_kv(scn);
   int churn = scn == MR_SCN_RELIABLE_CHURN_2C || scn == MR_SCN_UNRELIABLE_CHURN_2C;
-  uint32_t cap = fig8 ? 2048 : kv ? (scn == MR_SCN_KV_CONCURRENT_3A ? 8192 : 2048)
+  uint32_t cap = fig8 ? 2048 : kv ? mr_kv_log_cap(scn)
                : churn ? 4096 : scn == MR_SCN_UNRELIABLE_AGREE_2C ? 1024 : 0;
   c->log_cap = cap ? cap : 256;
   c->apply_cap = cap ? cap : (snap ? 1024 : 512);
@@ -207,6 +211,7 @@ int mr_batch_create(const mr_cfg* cfg, mr_batch** out) {
   D.unrel_flag = (cfg->flags & MR_F_UNRELIABLE) ? 1u : 0u;
   D.safety = (cfg->flags & MR_F_SAFETY) ? 1u : 0u;
   D.bugs = cfg->flags & (MR_F_BUG_VOTE_TWICE | MR_F_BUG_VOTE_STALE);
+  D.links = kv_gen(cfg->scenario).part ? 1u : 0u;  // server-link cuts (CS_CUT) can exist
   D.trace_clusters = (cfg->flags & MR_F_TRACE) ? cfg->trace_clusters : 0u;
   D.trace_cap = cfg->trace_cap;
   D.scenario = scn;
@@ -238,9 +243,7 @@ int mr_batch_create(const mr_cfg* cfg, mr_batch** out) {
   add(&D.pay, C * M * K);
   add(&D.stor, C * cfg->apply_cap);
   // scenario-only arrays: spawned tester threads, kvraft servers, churn values
-  static const uint8_t k_thr[MR_SCN_COUNT_] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 64,
-                                               0, 4, 4, 0, 0, 0, 0, 0, 0, 6, 6, 6, 11, 11};
-  D.nthr = k_thr[scn];
+  D.nthr = nthr(scn);
   if (D.nthr) add(&D.kt32, (size_t)KT__N * D.nthr * C);
   if (is_svc(scn)) add(&D.kv32, (size_t)KVREC * n * C);
   if (is_ctrl(scn)) {

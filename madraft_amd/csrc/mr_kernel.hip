@@ -267,6 +267,12 @@ DI void rescan_min(const Dev& D, X& x) {
   x.mslot = bs;
 }
 
+// server-server link i~j cut by disconnect2 (kvraft partitions); clerk links stay up
+DI bool link_cut(const Dev& D, X& x, uint32_t a, uint32_t b) {
+  if (!D.links || a >= CLERK_HOST || b >= CLERK_HOST) return false;
+  return (CS(CS_CUT + (a >> 2)) >> (8u * (a & 3u) + b)) & 1u;
+}
+
 // madsim net send from node `src` (whose state is `s`) (tester.rs:127-137,
 // :147-149). Returns the slot or -1 if the message is dropped.
 DI int net_send(const Dev& D, X& x, uint32_t src, uint32_t& nctr, uint32_t dst, uint32_t type,
@@ -274,7 +280,7 @@ DI int net_send(const Dev& D, X& x, uint32_t src, uint32_t& nctr, uint32_t dst, 
                 uint32_t k) {
   uint32_t seq = x.msgs_sent++;
   uint32_t ctr = nctr++;
-  if (!bit(x.conn, src) || !bit(x.conn, dst)) { CADD(CNT_DROP_CLOG, 1u); return -1; }
+  if (!bit(x.conn, src) || !bit(x.conn, dst) || link_cut(D, x, src, dst)) { CADD(CNT_DROP_CLOG, 1u); return -1; }
   uint32_t w0, w1;
   philox(D, x, ctr, src, ST_NET, w0, w1);
   if (w0 < net_loss(x)) { CADD(CNT_DROP_LOSS, 1u); return -1; }
@@ -533,7 +539,7 @@ DI void node_event(const Dev& D, X& x, bool is_msg, uint32_t tnode, uint32_t slo
   const uint32_t others = ((1u << D.n) - 1u) & ~(1u << me);
   if (is_msg) {
     kind = type;
-    if (!bit(x.alive, me) || !bit(x.conn, me) || !bit(x.conn, src)) {
+    if (!bit(x.alive, me) || !bit(x.conn, me) || !bit(x.conn, src) || link_cut(D, x, src, me)) {
       CADD(CNT_DROP_DELIVER, 1u);
       rec_node(D, x, 0, 16, me, seq, d);
       PROF(P_DROP);

@@ -93,6 +93,7 @@ typedef struct {
 } OClerk;
 typedef struct {
   uint32_t tid, live, pc, j, cli, tctr, gen;
+  uint32_t kind, perm; /* kind 1 = generic_test partitioner (perm: its shuffled `all`, 4 bits/server) */
   /* churn client (tests.rs:763-797) */
   uint64_t xv; uint32_t idx, has, toi, nval;
   /* one() task (tester.rs:216-262) */
@@ -125,6 +126,7 @@ typedef struct {
   uint64_t* cval; uint32_t* cidx; /* churn values [3][CHURN_VCAP] + their indices */
   uint32_t ctrl_mode, nops, ncfg[MR_MAX_NODES];
   uint32_t lring[32]; /* MR_F_SAFETY: (term << 4) | leader + 1 by term mod 32 */
+  uint8_t link[MR_MAX_NODES]; /* server links (connect2/disconnect2): bit j of link[i] = i~j */
   OCfg* cfgs; /* [MR_MAX_NODES][CFG_CAP] */
   OOp* ops;   /* [OP_CAP] */
   uint32_t churn_stop;
@@ -228,6 +230,11 @@ static void reset_timer(OSim* s, uint32_t d) {
 /* network (madsim net: tester.rs:127-137 config, :147-149 stat)        */
 /* ------------------------------------------------------------------ */
 static int host_conn(OSim* s, uint32_t h) { return h < CLERK_HOST ? s->nd[h].conn : 1; }
+/* the link between two hosts (madsim connect2/disconnect2, kvraft/tester.rs:88-124):
+ * server-server links are symmetric bits; clerk links are always up here */
+static int link_up(OSim* s, uint32_t a, uint32_t b) {
+  return a >= CLERK_HOST || b >= CLERK_HOST || ((s->link[a] >> b) & 1u);
+}
 static uint32_t* host_nctr(OSim* s, uint32_t h) {
   if (h < CLERK_HOST) return &s->nd[h].n_ctr;
   for (uint32_t k = 0; k < CK_SLOTS; k++)
@@ -241,7 +248,7 @@ static void net_send(OSim* s, uint32_t src, uint32_t dst, OMsg* m) {
   s->r.msgs_sent++;
   uint32_t ctr[4] = {(*host_nctr(s, src))++, src, ST_NET, 0}, w[4];
   mro_philox4x32_10(ctr, s->key, w);
-  if (!host_conn(s, src) || !host_conn(s, dst)) { s->r.drop_clog++; return; }
+  if (!host_conn(s, src) || !host_conn(s, dst) || !link_up(s, src, dst)) { s->r.drop_clog++; return; }
   if (w[0] < s->loss) { s->r.drop_loss++; return; }
   if (s->inflight >= s->cfg.msg_slots) { s->r.drop_overflow++; return; }
   if (seq >= (1u << 25)) t_fail(s, MR_FAIL_SIM_CAPACITY); /* SEMANTICS §3, §9 */
@@ -563,7 +570,7 @@ static void deliver(OSim* s, OMsg* m) {
   uint32_t me = m->dst;
   if (me >= CLERK_HOST) { clerk_deliver(s, m); return; }
   ONode* d = &s->nd[me];
-  if (!d->alive || !d->conn || !host_conn(s, m->src)) {
+  if (!d->alive || !d->conn || !host_conn(s, m->src) || !link_up(s, m->src, me)) {
     s->r.drop_deliver++;
     rec_node(s, 0, 16, me, m->seq);
     return;
@@ -1371,6 +1378,59 @@ finish:
   thr_finish(s, slot);
 }
 
+/* kvraft/tester.rs:88-124: connect2 / disconnect2 of every (i in p1, j in p2), both ways */
+static void set_link(OSim* s, uint32_t i, uint32_t j, int up) {
+  if (up) { s->link[i] |= (uint8_t)(1u << j); s->link[j] |= (uint8_t)(1u << i); }
+  else { s->link[i] &= (uint8_t)~(1u << j); s->link[j] &= (uint8_t)~(1u << i); }
+}
+static void t_partition(OSim* s, uint32_t p1, uint32_t p2) { /* masks of servers; tester.rs:112-122 */
+  for (uint32_t i = 0; i < s->n; i++) {
+    if (!((p1 >> i) & 1u)) continue;
+    for (uint32_t j = 0; j < s->n; j++) if ((p2 >> j) & 1u) set_link(s, i, j, 0);
+    for (uint32_t j = 0; j < s->n; j++) if ((p1 >> j) & 1u) set_link(s, i, j, 1);
+  }
+  for (uint32_t i = 0; i < s->n; i++) {
+    if (!((p2 >> i) & 1u)) continue;
+    for (uint32_t j = 0; j < s->n; j++) if ((p1 >> j) & 1u) set_link(s, i, j, 0);
+    for (uint32_t j = 0; j < s->n; j++) if ((p2 >> j) & 1u) set_link(s, i, j, 1);
+  }
+}
+static void t_connect_all(OSim* s) { memset(s->link, 0xFF, sizeof s->link); } /* tester.rs:106-110 */
+
+static uint32_t thr_range(OSim* s, OThr* t, uint32_t lo, uint32_t hi) { /* rng.gen_range(lo..hi) */
+  uint32_t ctr[4] = {t->tctr++, t->tid, ST_TESTER, 0}, w[4];
+  mro_philox4x32_10(ctr, s->key, w);
+  return u_range(w[0], lo, hi);
+}
+
+/* the partitioner task of generic_test (kvraft/tests.rs:135-157): while !done,
+ * shuffle `all` (rand 0.8 SliceRandom::shuffle: i = n-1..1, swap(i, gen_range(0..i+1))),
+ * split at gen_range(0..n), partition, sleep RAFT_ELECTION_TIMEOUT + gen_range(0..200) ms */
+static void part_step(OSim* s, uint32_t slot) {
+  OThr* t = &s->th[slot];
+  if (s->kv_done) {
+    rec_simple(s, 2, t->tid & 0xFFu);
+    thr_finish(s, slot);
+    return;
+  }
+  uint32_t n = s->n, a[MR_MAX_NODES];
+  for (uint32_t i = 0; i < n; i++) a[i] = (t->perm >> (4 * i)) & 15u;
+  for (uint32_t i = n - 1; i >= 1; i--) {
+    uint32_t j = thr_range(s, t, 0, i + 1), x = a[i];
+    a[i] = a[j]; a[j] = x;
+  }
+  uint32_t k = thr_range(s, t, 0, n), left = 0, right = 0;
+  t->perm = 0;
+  for (uint32_t i = 0; i < n; i++) {
+    t->perm |= a[i] << (4 * i);
+    if (i < k) left |= 1u << a[i]; else right |= 1u << a[i];
+  }
+  t_partition(s, left, right);
+  uint32_t ms = thr_range(s, t, 0, 200);
+  rec_simple(s, 2, t->tid & 0xFFu);
+  thr_wake(s, slot, s->now + 1000000u + 1000u * ms);
+}
+
 /* ---- raft tests with spawn_local (tests.rs:662-686, 743-856) ---- */
 static uint64_t thr_entry(OSim* s, OThr* t) { /* random.gen_entry() on the thread's stream */
   uint32_t ctr[4] = {t->tctr++, t->tid, ST_TESTER, 0}, w[4];
@@ -1462,7 +1522,10 @@ static void client_step(OSim* s, uint32_t slot) {
     case MR_SCN_UNRELIABLE_AGREE_2C: one_thr_step(s, slot); break;
     case MR_SCN_CTRL_BASIC_4A:
     case MR_SCN_CTRL_MULTI_4A: ctl_client_step(s, slot); break;
-    default: kv_client_step(s, slot); break;
+    default:
+      if (s->th[slot].kind == 1) part_step(s, slot);
+      else kv_client_step(s, slot);
+      break;
   }
 }
 
@@ -1579,17 +1642,47 @@ static uint32_t main_call(OSim* s, uint32_t op, uint32_t key, uint32_t elem) { /
   }
 }
 
-static void scn_kv_generic(OSim* s, uint32_t nclients, int unreliable) { /* kvraft/tests.rs:65-220 */
+/* kvraft/tester.rs:153-169: the KV server's state machine is volatile (rebuilt by
+ * re-applying the log from the snapshot); its Raft state persists (SEMANTICS §9) */
+static void t_shutdown_server(OSim* s, uint32_t i) { t_crash1(s, i); }
+static void t_start_server(OSim* s, uint32_t i) {
+  t_start1(s, i);
+  memset(s->kv_n[i], 0, sizeof s->kv_n[i]);
+  s->kv_ok[i] = 0;
+  memset(s->kv_dedup[i], 0, sizeof s->kv_dedup[i]);
+}
+
+static void scn_kv_generic(OSim* s, uint32_t nclients, int unreliable, int crash,
+                           int partitions) { /* kvraft/tests.rs:65-220 */
   t_new(s, 0); /* Tester::new (kvraft/tester.rs:27-56): start_server for every server */
   if (unreliable) t_set_unreliable(s, 1);
   s->kv_mode = 1;
   s->th[0].live = 1;
   memset(&s->ck[0], 0, sizeof s->ck[0]); /* ck = make_client(&t.all()): clerk 0 */
+  uint32_t ps = 1 + nclients; /* the partitioner's slot */
   for (uint32_t i = 0; i < 3; i++) {
     s->kv_done = 0;
     for (uint32_t cli = 0; cli < nclients; cli++) kv_spawn(s, 1 + cli, 1 + nclients * i + cli, cli);
+    if (partitions) {
+      t_sleep(s, 1000000u);
+      thr_spawn(s, ps, 1 + 3 * nclients + i);
+      s->th[ps].kind = 1;
+      s->ck[ps].id = 0xFFFFu; /* no clerk */
+      for (uint32_t k = 0; k < s->n; k++) s->th[ps].perm |= k << (4 * k); /* t.all() */
+    }
     t_sleep(s, 5000000u);
     s->kv_done = 1;
+    if (partitions) {
+      t_join(s, ps);
+      t_connect_all(s);
+      t_sleep(s, ELECTION_US);
+    }
+    if (crash) {
+      for (uint32_t k = 0; k < s->n; k++) t_shutdown_server(s, k);
+      t_sleep(s, ELECTION_US);
+      for (uint32_t k = 0; k < s->n; k++) t_start_server(s, k);
+      t_connect_all(s);
+    }
     for (uint32_t cli = 0; cli < nclients; cli++) {
       t_join(s, 1 + cli);
       uint32_t j = s->th[1 + cli].j;
@@ -1850,9 +1943,16 @@ static int run_scenario(OSim* s) {
     case MR_SCN_UNRELIABLE_CHURN_2C: scn_churn(s, 1); break;
     case MR_SCN_CTRL_BASIC_4A: scn_ctrl_basic(s); break;
     case MR_SCN_CTRL_MULTI_4A: scn_ctrl_multi(s); break;
-    case MR_SCN_KV_BASIC_3A: scn_kv_generic(s, 1, 0); break;
-    case MR_SCN_KV_CONCURRENT_3A: scn_kv_generic(s, 5, 0); break;
-    case MR_SCN_KV_UNRELIABLE_3A: scn_kv_generic(s, 5, 1); break;
+    case MR_SCN_KV_BASIC_3A: scn_kv_generic(s, 1, 0, 0, 0); break;
+    case MR_SCN_KV_CONCURRENT_3A: scn_kv_generic(s, 5, 0, 0, 0); break;
+    case MR_SCN_KV_UNRELIABLE_3A: scn_kv_generic(s, 5, 1, 0, 0); break;
+    case MR_SCN_KV_MANY_PARTITIONS_ONE_CLIENT_3A: scn_kv_generic(s, 1, 0, 0, 1); break;
+    case MR_SCN_KV_MANY_PARTITIONS_MANY_CLIENTS_3A: scn_kv_generic(s, 5, 0, 0, 1); break;
+    case MR_SCN_KV_PERSIST_ONE_CLIENT_3A: scn_kv_generic(s, 1, 0, 1, 0); break;
+    case MR_SCN_KV_PERSIST_CONCURRENT_3A: scn_kv_generic(s, 5, 0, 1, 0); break;
+    case MR_SCN_KV_PERSIST_CONCURRENT_UNRELIABLE_3A: scn_kv_generic(s, 5, 1, 1, 0); break;
+    case MR_SCN_KV_PERSIST_PARTITION_3A: scn_kv_generic(s, 5, 0, 1, 1); break;
+    case MR_SCN_KV_PERSIST_PARTITION_UNRELIABLE_3A: scn_kv_generic(s, 5, 1, 1, 1); break;
     default: return -1;
   }
   return 0;
@@ -1911,6 +2011,7 @@ static void sim_reset(OSim* s, uint64_t cluster) {
   memset(s->ck, 0, sizeof s->ck); memset(s->th, 0, sizeof s->th); s->churn_stop = 0;
   s->ctrl_mode = 0; s->nops = 0;
   memset(s->lring, 0, sizeof s->lring);
+  memset(s->link, 0xFF, sizeof s->link);
   for (uint32_t i = 0; i < MR_MAX_NODES; i++) { /* the initial config, num 0 */
     s->ncfg[i] = 1;
     memset(&s->cfgs[i * CFG_CAP], 0, sizeof(OCfg));
@@ -1985,7 +2086,10 @@ static const char* k_names[MR_SCN_COUNT_] = {
     "unreliable_churn_2c", "snapshot_basic_2d", "snapshot_install_2d",
     "snapshot_install_unreliable_2d", "snapshot_install_crash_2d",
     "snapshot_install_unreliable_crash_2d", "figure_8_unreliable_crash", "basic_3a",
-    "concurrent_3a", "unreliable_3a", "basic_4a", "multi_4a"};
+    "concurrent_3a", "unreliable_3a", "basic_4a", "multi_4a",
+    "many_partitions_one_client_3a", "many_partitions_many_clients_3a", "persist_one_client_3a",
+    "persist_concurrent_3a", "persist_concurrent_unreliable_3a", "persist_partition_3a",
+    "persist_partition_unreliable_3a"};
 
 uint32_t mro_scenario_from_name(const char* name) {
   for (uint32_t i = 1; i < MR_SCN_COUNT_; i++)
@@ -1995,7 +2099,8 @@ uint32_t mro_scenario_from_name(const char* name) {
 
 int mro_cfg_init(mr_cfg* c, uint32_t scn) {
   static const uint8_t k_n[MR_SCN_COUNT_] = {0, 3, 3, 7, 5, 3, 5, 3, 3, 5, 3, 3, 5, 3,
-                                             5, 5, 5, 5, 5, 3, 3, 3, 3, 3, 5, 5, 5, 5, 3, 3};
+                                             5, 5, 5, 5, 5, 3, 3, 3, 3, 3, 5, 5, 5, 5, 3, 3,
+                                             5, 5, 5, 5, 5, 5, 5};
   if (scn == 0 || scn >= MR_SCN_COUNT_) return -1;
   memset(c, 0, sizeof *c);
   c->abi_version = MR_ABI_VERSION;
@@ -2007,9 +2112,9 @@ int mro_cfg_init(mr_cfg* c, uint32_t scn) {
   int fig8 = scn == MR_SCN_FIGURE_8_2C || scn == MR_SCN_FIGURE_8_UNRELIABLE_2C ||
              scn == MR_SCN_FIGURE_8_UNRELIABLE_CRASH;
   int snap = scn >= MR_SCN_SNAPSHOT_BASIC_2D && scn <= MR_SCN_SNAPSHOT_INSTALL_UNRELIABLE_CRASH_2D;
-  int kv = scn >= MR_SCN_KV_BASIC_3A && scn <= MR_SCN_KV_UNRELIABLE_3A;
+  int kv = mr_scn_is_kv(scn);
   int churn = scn == MR_SCN_RELIABLE_CHURN_2C || scn == MR_SCN_UNRELIABLE_CHURN_2C;
-  uint32_t cap = fig8 ? 2048 : kv ? (scn == MR_SCN_KV_CONCURRENT_3A ? 8192 : 2048)
+  uint32_t cap = fig8 ? 2048 : kv ? mr_kv_log_cap(scn)
                : churn ? 4096 : scn == MR_SCN_UNRELIABLE_AGREE_2C ? 1024 : 0;
   c->log_cap = cap ? cap : 256;
   c->apply_cap = cap ? cap : (snap ? 1024 : 512);
