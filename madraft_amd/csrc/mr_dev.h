@@ -92,15 +92,22 @@ enum : uint32_t {
   KT_TID, KT_LIVE, KT_PC, KT_J, KT_CLI, KT_TCTR, KT_WAKE, KT_ID, KT_LH, KT_SEQ, KT_TAG, KT_NCTR,
   KT_WAITING, KT_GOT, KT_RSTAT, KT_RHINT, KT_RVAL, KT_OP, KT_KEY, KT_ELEM,
   KT_KIND,  // 1 = generic_test partitioner (KT_PERM: its shuffled `all`, 4 bits per server)
-  KT_PERM, KT__N
+  KT_PERM,
+  KT_RVH0, KT_RVH1,  // the reply's value hash
+  KT_HL0, KT_HL1,    // generic_test client: hash of its predicted value `last`
+  KT__N
 };
 constexpr uint32_t KT_W = KT_ID;
 constexpr uint32_t JOIN_ALL = 0xFFFFFFFEu;
 constexpr uint32_t CHURN_VCAP = 512;  // values one churn client may record (tests.rs:763-797)
-// kv32 [C][n][KVREC]: per-server KV state: n[key] at 0..7, ok mask at 8, dedup[clerk] at
-// 16..31, pending request p at 32 + 4p: {index (0 = free), clerk | seq24 << 5 |
-// ready << 29 | status << 30, tag, value}
-constexpr uint32_t KVR_N = 0, KVR_OK = 8, KVR_NCFG = 9, KVR_DEDUP = 16, KVR_PEND = 32, KVREC = 64;
+// kv32 [C][n][KVREC]: per-server KV state (SEMANTICS §9): dedup[clerk] at 0..127, pending
+// request p at 128 + 8p: {index (0 = free), clerk | ready << 8 | status << 9 | host << 16,
+// seq, tag, value, hash lo, hash hi, -}, the shard_ctrler config count at 192, and key k at
+// 256 + 8k: {hash lo, hash hi, byte length, appender 0..4 (cli + 1 | count << 8 | bad << 31)}
+constexpr uint32_t KVR_DEDUP = 0, KVR_PEND = 128, KVR_NCFG = 192, KVR_KEYS = 256, KVREC = 768;
+constexpr uint32_t KV_KEYS = 64, KV_KW = 8, KV_APP = 5, MAX_CLERKS = 128;
+constexpr uint32_t KV_ALL = 0xFFFFFFu;  // Get elem: appenders 0..4, packed
+constexpr uint64_t KV_HP = 0x100000001B3ull;  // value hash multiplier
 // ---- shard_ctrler (SEMANTICS §10): per-server append-only config store and a
 // per-cluster table of clerk operations (the log command names an operation)
 constexpr uint32_t N_SHARDS = 10;  // shard_ctrler/mod.rs:9

@@ -528,7 +528,8 @@ DI void node_event(const Dev& D, X& x, bool is_msg, uint32_t tnode, uint32_t slo
     PROF(P_DECODE);
     if constexpr (KV) {
       if (me >= CLERK_HOST) {  // KV_REP at a clerk host
-        clerk_deliver(D, x, me, src, mterm, ma, mb, mc, seq);
+        const uint64_t mv = ((uint64_t)MS32(MF_V + 1, slot) << 32) | MS32(MF_V, slot);
+        clerk_deliver(D, x, me, src, inc, mterm, ma, mb, mc, mv, seq);
         return;
       }
     }
@@ -554,7 +555,7 @@ DI void node_event(const Dev& D, X& x, bool is_msg, uint32_t tnode, uint32_t slo
     }
     if constexpr (KV) {
       if (type == M_KV_REQ) {  // no Raft term: handled before the step-down rule
-        kv_request(D, x, me, d, src, mterm, ma, mb, mc);
+        kv_request(D, x, me, d, src, inc, mterm, ma, mb, mc);
         if (x.code != RUN) return;
         store_node(D, x, me, d);
         rec_node(D, x, 0, type, me, seq, d);
@@ -791,7 +792,7 @@ DI void t_crash1(const Dev& D, X& x, uint32_t i) {  // tester.rs:329-333
   set_timer(x, i, INF_T);
   if (D.kv32) {  // its RPC handler tasks die with it: pending requests are dropped
     uint4* pp = reinterpret_cast<uint4*>(D.kv32 + ((size_t)x.c * D.n + i) * KVREC + KVR_PEND);
-    for (uint32_t p = 0; p < KV_PEND; p++) pp[p] = make_uint4(0u, 0u, 0u, 0u);
+    for (uint32_t p = 0; p < 2 * KV_PEND; p++) pp[p] = make_uint4(0u, 0u, 0u, 0u);
   }
 }
 DI void t_start1(const Dev& D, X& x, uint32_t i) {  // tester.rs:293-327, raft.rs:108-122

@@ -42,11 +42,15 @@ enum { R_F = 0, R_C = 1, R_L = 2, R_DOWN = 3 };
 enum { M_RV_REQ = 1, M_RV_REP, M_AE_REQ, M_AE_REP, M_IS_REQ, M_IS_REP, M_KV_REQ, M_KV_REP };
 enum { KV_GET = 0, KV_PUT = 1, KV_APPEND = 2 };
 enum { KV_OK = 0, KV_WRONG_LEADER = 1, KV_FAILED = 2 };
-#define CLERK_HOST 8u   /* clerk c is host 8 + c (SEMANTICS §9) */
-#define MAX_CLERKS 16u
+#define CLERK_HOST 8u   /* the clerk of thread slot k is host 8 + k (SEMANTICS §9) */
+#define MAX_CLERKS 128u /* clerk ids (make_client order) */
+#define KV_KEYS 64u     /* keys a KV server may hold */
+#define KV_APP 5u       /* distinct appenders tracked per key */
+#define KV_ALL 0xFFFFFFu /* Get elem: the states of appenders 0..4, packed */
+#define KV_HP 0x100000001B3ull /* value hash multiplier (SEMANTICS §9) */
 #define KV_SLOTS 6u     /* thread / clerk slots: 0 = main + ck, 1 + cli = client cli */
 #define KV_PEND 8u
-#define CK_SLOTS 16u    /* clerk slots (thread slot k owns clerk k): ck + up to 10 concurrent clerks */
+#define CK_SLOTS 24u    /* clerk slots (thread slot k owns clerk k, host 8 + k) */
 #define MAX_THR 64u     /* tester thread slots (unreliable_agree_2c: concurrent one() tasks) */
 #define JOIN_ALL 0xFFFFFFFEu
 #define CHURN_VCAP 512u /* values a churn client may record (tests.rs:763-797) */
@@ -88,18 +92,22 @@ typedef struct { uint64_t key; uint32_t ref; uint32_t gen; } HEnt;
 
 /* kvraft clerk (kvraft/client.rs ClerkCore) and the tester thread that owns it */
 typedef struct {
-  uint32_t id, lh, seq, tag, nctr, waiting, got, rstat, rhint, rval;
+  uint32_t id, lh, seq, tag, nctr, waiting, got, rstat, rhint, rval; uint64_t rvh;
   uint32_t op, key, elem;
 } OClerk;
 typedef struct {
   uint32_t tid, live, pc, j, cli, tctr, gen;
-  uint32_t kind, perm; /* kind 1 = generic_test partitioner (perm: its shuffled `all`, 4 bits/server) */
+  uint32_t kind, perm;
+  uint64_t hlast; /* generic_test client: hash of its predicted value `last` */ /* kind 1 = generic_test partitioner (perm: its shuffled `all`, 4 bits/server) */
   /* churn client (tests.rs:763-797) */
   uint64_t xv; uint32_t idx, has, toi, nval;
   /* one() task (tester.rs:216-262) */
   uint64_t cmd; uint32_t t0, starts, index, t1, ph, expected, retry;
 } OThr;
-typedef struct { uint32_t used, idx, clerk, seq, tag, ready, status, value; } OPend;
+typedef struct { uint32_t used, idx, clerk, seq, tag, ready, status, value, host; uint64_t vh; } OPend;
+/* a key's value (SEMANTICS §9): the hash of its token sequence, its byte length, and
+ * per appender (cli + 1 | count << 8 | bad << 31) for the append-order checks */
+typedef struct { uint64_t h; uint32_t len; uint32_t app[KV_APP]; } OKey;
 /* Config (shard_ctrler/msg.rs:11-18): groups sorted by gid; a server list is
  * packed as len | a0 << 8 | a1 << 16 | a2 << 24 (addrs! takes `as u8`) */
 typedef struct { uint32_t num, shards[N_SHARDS], ng, gid[CFG_G], addr[CFG_G]; } OCfg;
@@ -120,7 +128,7 @@ typedef struct {
   uint8_t* mask; uint64_t* sval; uint32_t slen[MR_MAX_NODES];
   /* kvraft (SEMANTICS §8-9) */
   uint32_t kv_mode, kv_done, next_tid, mwake, main_join;
-  uint32_t kv_n[MR_MAX_NODES][8], kv_ok[MR_MAX_NODES], kv_dedup[MR_MAX_NODES][MAX_CLERKS];
+  OKey kv[MR_MAX_NODES][KV_KEYS]; uint32_t kv_dedup[MR_MAX_NODES][MAX_CLERKS];
   OPend pend[MR_MAX_NODES][KV_PEND];
   OClerk ck[CK_SLOTS]; OThr th[MAX_THR];
   uint64_t* cval; uint32_t* cidx; /* churn values [3][CHURN_VCAP] + their indices */
@@ -237,10 +245,7 @@ static int link_up(OSim* s, uint32_t a, uint32_t b) {
 }
 static uint32_t* host_nctr(OSim* s, uint32_t h) {
   if (h < CLERK_HOST) return &s->nd[h].n_ctr;
-  for (uint32_t k = 0; k < CK_SLOTS; k++)
-    if (s->ck[k].id == h - CLERK_HOST) return &s->ck[k].nctr;
-  t_fail(s, MR_FAIL_SIM_BAD_PROGRAM);
-  return NULL;
+  return &s->ck[h - CLERK_HOST].nctr;
 }
 
 static void net_send(OSim* s, uint32_t src, uint32_t dst, OMsg* m) {
@@ -383,36 +388,70 @@ static uint32_t ctl_apply(OSim* s, uint32_t me, uint32_t clerk, uint32_t seq, ui
   return 0;
 }
 
+static uint32_t ndig(uint32_t v) { uint32_t d = 1; while (v >= 10) { v /= 10; d++; } return d; }
+/* a Put value token: 0 = "", t < 2^20 = the decimal string of t - 1, else one letter */
+static uint32_t put_len(uint32_t t) { return t == 0 ? 0 : t < (1u << 20) ? ndig(t - 1) : 1; }
+
+/* the state of appender `cli` of a key: count | ok << 31 (ok: its tokens arrived in order, once) */
+static uint32_t kv_app_state(const OKey* k, uint32_t cli) {
+  for (uint32_t a = 0; a < KV_APP; a++)
+    if ((k->app[a] & 0xFFu) == cli + 1) return ((k->app[a] >> 8) & 0xFFFFFFu) | ((~k->app[a] >> 31) << 31);
+  return 1u << 31;
+}
+
+/* Kv::apply (kvraft/server.rs:74-87, the build's completion; SEMANTICS §9) of log entry i
+ * (command v) at server me: values are token sequences kept as (hash, length, appenders) */
 static void kv_apply(OSim* s, uint32_t me, uint32_t i, uint64_t v) {
-  uint32_t op = (uint32_t)(v >> 56) & 3u, key = (uint32_t)(v >> 53) & 7u;
-  uint32_t clerk = (uint32_t)(v >> 48) & 31u, seq = (uint32_t)(v >> 24) & 0xFFFFFFu;
+  uint32_t op = (uint32_t)(v >> 61) & 3u, key = (uint32_t)(v >> 55) & 63u;
+  uint32_t clerk = (uint32_t)(v >> 48) & 127u, seq = (uint32_t)(v >> 24) & 0xFFFFFFu;
   uint32_t elem = (uint32_t)v & 0xFFFFFFu, out = 0;
-  uint32_t* n = &s->kv_n[me][key];
+  uint64_t outh = 0;
+  OKey* k = &s->kv[me][key];
   int query = op == KV_GET;
   if (s->ctrl_mode) { /* shard_ctrler: elem = the operation's id */
     out = ctl_apply(s, me, clerk, seq, elem);
     query = s->ops[elem].type == CT_QUERY;
   } else if (op == KV_GET) {
-    out = *n | (((s->kv_ok[me] >> key) & 1u) << 31);
+    outh = k->h;
+    if (elem == KV_ALL) { /* appenders 0..4: count (5 bits) | ok << 5 each */
+      for (uint32_t c = 0; c < KV_APP; c++) {
+        uint32_t st = kv_app_state(k, c), n = st & 0xFFFFFFu;
+        out |= ((n > 31 ? 31 : n) | ((n <= 31 && (st >> 31)) ? 32u : 0u)) << (6 * c);
+      }
+    } else {
+      out = kv_app_state(k, elem);
+    }
   } else if (seq > s->kv_dedup[me][clerk]) {
-    if (op == KV_PUT) { *n = 0; s->kv_ok[me] |= 1u << key; }
-    else if (((s->kv_ok[me] >> key) & 1u) && elem == *n) (*n)++;
-    else s->kv_ok[me] &= ~(1u << key);
+    if (op == KV_PUT) { /* elem = the value's token (0 = "") */
+      memset(k, 0, sizeof *k);
+      if (elem) { k->h = (elem + 1ull) * 0x9E3779B97F4A7C15ull; k->len = put_len(elem); }
+    } else { /* Append of token "x {cli} {j} y": elem = cli << 19 | j */
+      uint32_t cli = elem >> 19, j = elem & 0x7FFFFu, a = 0;
+      while (a < KV_APP && (k->app[a] & 0xFFu) != cli + 1 && (k->app[a] & 0xFFu) != 0) a++;
+      if (a == KV_APP) t_fail(s, MR_FAIL_SIM_CAPACITY);
+      uint32_t w = k->app[a], n = (w >> 8) & 0xFFFFFFu;
+      if (!(w >> 31) && n == j) w = (cli + 1) | ((n + 1) << 8);
+      else w = (cli + 1) | (n << 8) | (1u << 31);
+      k->app[a] = w;
+      k->h = k->h * KV_HP + elem + 1;
+      k->len += 5 + ndig(cli) + ndig(j);
+    }
     s->kv_dedup[me][clerk] = seq;
   }
   for (uint32_t p = 0; p < KV_PEND; p++) { /* answered at the end of the event (kv_flush) */
     OPend* q = &s->pend[me][p];
     if (!q->used || q->ready || q->idx != i) continue;
     int ok = q->clerk == clerk && q->seq == seq;
-    q->ready = 1; q->status = ok ? KV_OK : KV_FAILED; q->value = (ok && query) ? out : 0;
+    q->ready = 1; q->status = ok ? KV_OK : KV_FAILED;
+    q->value = (ok && query) ? out : 0; q->vh = (ok && query) ? outh : 0;
   }
 }
 
-static void kv_send_rep(OSim* s, uint32_t src, uint32_t dst, uint32_t tag, uint32_t status,
-                        uint32_t hint, uint32_t value) {
+static void kv_send_rep(OSim* s, uint32_t src, uint32_t dst, uint32_t clerk, uint32_t tag,
+                        uint32_t status, uint32_t hint, uint32_t value, uint64_t vh) {
   OMsg m;
-  m.type = M_KV_REP; m.inc = 0; m.term = tag; m.a = status; m.b = hint; m.c = value;
-  m.k = 0; m.v = 0;
+  m.type = M_KV_REP; m.inc = (uint8_t)clerk; m.term = tag; m.a = status; m.b = hint; m.c = value;
+  m.k = 0; m.v = vh;
   net_send(s, src, dst, &m);
 }
 
@@ -422,7 +461,7 @@ static void kv_flush(OSim* s, uint32_t me) {
     OPend* q = &s->pend[me][p];
     if (!q->used || !q->ready) continue;
     q->used = 0; q->ready = 0;
-    kv_send_rep(s, me, CLERK_HOST + q->clerk, q->tag, q->status, me, q->value); /* hint = server */
+    kv_send_rep(s, me, q->host, q->clerk, q->tag, q->status, me, q->value, q->vh); /* hint = server */
   }
 }
 
@@ -531,18 +570,15 @@ static void thr_wake(OSim* s, uint32_t slot, uint32_t t);
 
 /* KV_REP at a clerk host: wake the clerk's thread if it waits for this tag */
 static void clerk_deliver(OSim* s, OMsg* m) {
-  uint32_t id = m->dst - CLERK_HOST;
-  OClerk* c = NULL;
-  uint32_t slot = 0;
-  for (uint32_t k = 0; k < CK_SLOTS; k++)
-    if (s->th[k].live && s->ck[k].id == id) { c = &s->ck[k]; slot = k; }
+  uint32_t slot = m->dst - CLERK_HOST;
+  OClerk* c = &s->ck[slot];
   if (!host_conn(s, m->src)) { s->r.drop_deliver++; rec_host(s, 16, m->dst, m->seq); return; }
-  if (!c || !c->waiting || c->got || m->term != c->tag) {
+  if (!s->th[slot].live || c->id != m->inc || !c->waiting || c->got || m->term != c->tag) {
     s->r.drop_stale++;
     rec_host(s, 17, m->dst, m->seq);
     return;
   }
-  c->got = 1; c->rstat = m->a; c->rhint = m->b; c->rval = m->c;
+  c->got = 1; c->rstat = m->a; c->rhint = m->b; c->rval = m->c; c->rvh = m->v;
   thr_wake(s, slot, s->now);
   rec_host(s, M_KV_REP, m->dst, m->seq);
 }
@@ -550,20 +586,22 @@ static void clerk_deliver(OSim* s, OMsg* m) {
 /* KV_REQ at server `me` (kvraft/server.rs:48-56 handler + :68-70 apply, SEMANTICS §9) */
 static void kv_request(OSim* s, uint32_t me, OMsg* m) {
   ONode* d = &s->nd[me];
-  uint32_t clerk = m->src - CLERK_HOST;
+  uint32_t clerk = m->inc; /* the request names its clerk; the reply goes to the sending host */
   if (s->null_raft || d->role != R_L) {
-    kv_send_rep(s, me, m->src, m->term, KV_WRONG_LEADER, (me + 1) % s->n, 0);
+    kv_send_rep(s, me, m->src, clerk, m->term, KV_WRONG_LEADER, (me + 1) % s->n, 0, 0);
     return;
   }
   uint32_t p = 0;
   while (p < KV_PEND && s->pend[me][p].used) p++;
-  if (p == KV_PEND) { kv_send_rep(s, me, m->src, m->term, KV_FAILED, 0, 0); return; }
-  uint64_t cmd = (1ull << 63) | ((uint64_t)(m->a & 3u) << 56) | ((uint64_t)((m->a >> 2) & 7u) << 53) |
+  if (p == KV_PEND) { kv_send_rep(s, me, m->src, clerk, m->term, KV_FAILED, 0, 0, 0); return; }
+  /* command: 1 | op << 61 | key << 55 | clerk << 48 | seq24 << 24 | elem24 */
+  uint64_t cmd = (1ull << 63) | ((uint64_t)(m->a & 3u) << 61) | ((uint64_t)((m->a >> 2) & 63u) << 55) |
                  ((uint64_t)clerk << 48) | ((uint64_t)(m->b & 0xFFFFFFu) << 24) | (m->c & 0xFFFFFFu);
   log_put(s, d, d->last + 1, d->term, cmd); /* start(), raft.rs:238-244 */
   d->match[me] = d->last;
   OPend* q = &s->pend[me][p];
   q->used = 1; q->idx = d->last; q->clerk = clerk; q->seq = m->b & 0xFFFFFFu; q->tag = m->term;
+  q->host = m->src;
 }
 
 static void deliver(OSim* s, OMsg* m) {
@@ -1303,9 +1341,9 @@ static void clerk_send(OSim* s, uint32_t slot) { /* one call_timeout attempt, cl
   OClerk* c = &s->ck[slot];
   c->tag++;
   OMsg m;
-  m.type = M_KV_REQ; m.inc = 0; m.term = c->tag; m.a = c->op | (c->key << 2); m.b = c->seq;
-  m.c = c->elem; m.k = 0; m.v = 0;
-  net_send(s, CLERK_HOST + c->id, c->lh, &m);
+  m.type = M_KV_REQ; m.inc = (uint8_t)c->id; m.term = c->tag; m.a = c->op | (c->key << 2);
+  m.b = c->seq; m.c = c->elem; m.k = 0; m.v = 0;
+  net_send(s, CLERK_HOST + slot, c->lh, &m);
   c->waiting = 1; c->got = 0;
   thr_wake(s, slot, s->now + 500000u); /* Duration::from_millis(500) */
 }
@@ -1353,18 +1391,24 @@ static void kv_client_step(OSim* s, uint32_t slot) {
   OClerk* c = &s->ck[slot];
   for (;;) {
     switch (t->pc) {
-      case 0: clerk_begin(s, slot, KV_PUT, t->cli, 0); t->pc = 1; goto block; /* ck.put(&key, "") */
+      case 0: clerk_begin(s, slot, KV_PUT, t->cli, 0); t->hlast = 0; t->pc = 1; goto block; /* ck.put(&key, "") */
       case 1: if (!clerk_resume(s, slot)) goto block; t->pc = 2; break;
       case 2:
         if (s->kv_done) goto finish;
-        if (thr_bool(s, t, 0x80000000u)) { clerk_begin(s, slot, KV_APPEND, t->cli, t->j); t->pc = 3; }
-        else { clerk_begin(s, slot, KV_GET, t->cli, 0); t->pc = 4; }
+        if (thr_bool(s, t, 0x80000000u)) {
+          uint32_t e = (t->cli << 19) | t->j; /* "x {cli} {j} y"; last += &nv */
+          t->hlast = t->hlast * KV_HP + e + 1;
+          clerk_begin(s, slot, KV_APPEND, t->cli, e);
+          t->pc = 3;
+        } else {
+          clerk_begin(s, slot, KV_GET, t->cli, t->cli);
+          t->pc = 4;
+        }
         goto block;
       case 3: if (!clerk_resume(s, slot)) goto block; t->j++; t->pc = 2; break;
       case 4:
         if (!clerk_resume(s, slot)) goto block;
-        if (!((c->rval >> 31) && (c->rval & 0x7FFFFFFFu) == t->j))
-          t_fail(s, MR_FAIL_KV_GET_WRONG); /* kvraft/tests.rs:127 */
+        if (c->rvh != t->hlast) t_fail(s, MR_FAIL_KV_GET_WRONG); /* kvraft/tests.rs:127 */
         t->pc = 2;
         break;
       default: t_fail(s, MR_FAIL_SIM_BAD_PROGRAM);
@@ -1647,8 +1691,7 @@ static uint32_t main_call(OSim* s, uint32_t op, uint32_t key, uint32_t elem) { /
 static void t_shutdown_server(OSim* s, uint32_t i) { t_crash1(s, i); }
 static void t_start_server(OSim* s, uint32_t i) {
   t_start1(s, i);
-  memset(s->kv_n[i], 0, sizeof s->kv_n[i]);
-  s->kv_ok[i] = 0;
+  memset(s->kv[i], 0, sizeof s->kv[i]);
   memset(s->kv_dedup[i], 0, sizeof s->kv_dedup[i]);
 }
 
@@ -1686,7 +1729,7 @@ static void scn_kv_generic(OSim* s, uint32_t nclients, int unreliable, int crash
     for (uint32_t cli = 0; cli < nclients; cli++) {
       t_join(s, 1 + cli);
       uint32_t j = s->th[1 + cli].j;
-      uint32_t v = main_call(s, KV_GET, cli, 0);
+      uint32_t v = main_call(s, KV_GET, cli, cli); /* check_clnt_appends(cli, &v, j) */
       if (!(v >> 31)) t_fail(s, MR_FAIL_KV_APPEND_BAD);         /* kvraft/tests.rs:31-39 */
       if ((v & 0x7FFFFFFFu) < j) t_fail(s, MR_FAIL_KV_MISSING); /* kvraft/tests.rs:25-30 */
     }
@@ -2006,7 +2049,7 @@ static void sim_reset(OSim* s, uint64_t cluster) {
   for (uint32_t i = 0; i < s->n_free; i++) s->free_stack[i] = s->n_free - 1 - i;
   s->inflight = 0; s->heap_n = 0; s->t_ctr = 0;
   s->kv_mode = 0; s->kv_done = 0; s->mwake = 0; s->main_join = ~0u;
-  memset(s->kv_n, 0, sizeof s->kv_n); memset(s->kv_ok, 0, sizeof s->kv_ok);
+  memset(s->kv, 0, sizeof s->kv);
   memset(s->kv_dedup, 0, sizeof s->kv_dedup); memset(s->pend, 0, sizeof s->pend);
   memset(s->ck, 0, sizeof s->ck); memset(s->th, 0, sizeof s->th); s->churn_stop = 0;
   s->ctrl_mode = 0; s->nops = 0;
