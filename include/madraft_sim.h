@@ -83,17 +83,29 @@ enum mr_scenario {
   MR_SCN_KV_PERSIST_CONCURRENT_UNRELIABLE_3A = 34, /* kvraft/tests.rs:368-372 */
   MR_SCN_KV_PERSIST_PARTITION_3A = 35,             /* kvraft/tests.rs:374-378 */
   MR_SCN_KV_PERSIST_PARTITION_UNRELIABLE_3A = 36,  /* kvraft/tests.rs:380-384 */
+  MR_SCN_KV_UNRELIABLE_ONE_KEY_3A = 37,            /* kvraft/tests.rs:240-274 */
+  MR_SCN_KV_ONE_PARTITION_3A = 38,                 /* kvraft/tests.rs:276-342 */
+  /* kvraft 3B: services snapshot under maxraftstate = 1000 */
+  MR_SCN_KV_SNAPSHOT_RPC_3B = 39,                  /* kvraft/tests.rs:396-454 */
+  MR_SCN_KV_SNAPSHOT_SIZE_3B = 40,                 /* kvraft/tests.rs:456-492 */
+  MR_SCN_KV_SNAPSHOT_RECOVER_3B = 41,              /* kvraft/tests.rs:494-498 */
+  MR_SCN_KV_SNAPSHOT_RECOVER_MANY_CLIENTS_3B = 42, /* kvraft/tests.rs:500-504 */
+  MR_SCN_KV_SNAPSHOT_UNRELIABLE_3B = 43,           /* kvraft/tests.rs:506-510 */
+  MR_SCN_KV_SNAPSHOT_UNRELIABLE_RECOVER_3B = 44,   /* kvraft/tests.rs:512-516 */
+  MR_SCN_KV_SNAPSHOT_UNRELIABLE_RECOVER_CONCURRENT_PARTITION_3B = 45, /* kvraft/tests.rs:518-522 */
   MR_SCN_COUNT_
 };
 
 /* kvraft scenarios (generic_test and its variants) */
 static inline int mr_scn_is_kv(uint32_t s) {
   return (s >= MR_SCN_KV_BASIC_3A && s <= MR_SCN_KV_UNRELIABLE_3A) ||
-         (s >= MR_SCN_KV_MANY_PARTITIONS_ONE_CLIENT_3A && s <= MR_SCN_KV_PERSIST_PARTITION_UNRELIABLE_3A);
+         (s >= MR_SCN_KV_MANY_PARTITIONS_ONE_CLIENT_3A &&
+          s <= MR_SCN_KV_SNAPSHOT_UNRELIABLE_RECOVER_CONCURRENT_PARTITION_3B);
 }
 /* default log / apply capacity of a kvraft scenario (no snapshots: every op stays in the log) */
 static inline uint32_t mr_kv_log_cap(uint32_t s) {
-  return (s == MR_SCN_KV_BASIC_3A || s == MR_SCN_KV_UNRELIABLE_3A ||
+  if (s == MR_SCN_KV_SNAPSHOT_RECOVER_MANY_CLIENTS_3B) return 16384u;
+  return (s == MR_SCN_KV_BASIC_3A || s == MR_SCN_KV_UNRELIABLE_3A || s >= MR_SCN_KV_UNRELIABLE_ONE_KEY_3A ||
           s == MR_SCN_KV_PERSIST_CONCURRENT_UNRELIABLE_3A || s == MR_SCN_KV_PERSIST_PARTITION_UNRELIABLE_3A ||
           s == MR_SCN_KV_MANY_PARTITIONS_ONE_CLIENT_3A || s == MR_SCN_KV_PERSIST_ONE_CLIENT_3A) ? 2048u : 8192u;
 }
@@ -155,6 +167,11 @@ enum mr_fail {
   /* Raft invariants (MR_F_SAFETY; Raft paper Fig. 3), not reference panic sites */
   MR_FAIL_SAFETY_ELECTION = 42,   /* two leaders elected in one term */
   MR_FAIL_SAFETY_COMPLETENESS = 43, /* a new leader lacks a committed (applied) entry */
+  MR_FAIL_KV_LOG_SIZE = 44,          /* kvraft/tests.rs:208-215, :422-428, :475-481 */
+  MR_FAIL_KV_SNAPSHOT_SIZE = 45,     /* kvraft/tests.rs:483-489 */
+  MR_FAIL_KV_MINORITY_PROGRESS = 46, /* kvraft/tests.rs:315-319 */
+  MR_FAIL_KV_NO_COMPLETION = 47,     /* kvraft/tests.rs:333-337 */
+  MR_FAIL_KV_CHECK = 48,             /* kvraft/tester.rs:266-271 Clerk::check */
   /* simulator limits (not reference panics): a cluster that hits one is reported, never passed */
   MR_FAIL_SIM_CAPACITY = 60,      /* a log / apply / sequence capacity of the config was exceeded */
   MR_FAIL_SIM_EVENT_LIMIT = 61,   /* cfg.max_events processed without a verdict */

@@ -33,17 +33,23 @@ SCENARIOS = [
     "concurrent_3a", "unreliable_3a", "basic_4a", "multi_4a",
     "many_partitions_one_client_3a", "many_partitions_many_clients_3a", "persist_one_client_3a",
     "persist_concurrent_3a", "persist_concurrent_unreliable_3a", "persist_partition_3a",
-    "persist_partition_unreliable_3a",
+    "persist_partition_unreliable_3a", "unreliable_one_key_3a", "one_partition_3a",
+    "snapshot_rpc_3b", "snapshot_size_3b", "snapshot_recover_3b", "snapshot_recover_many_clients_3b",
+    "snapshot_unreliable_3b", "snapshot_unreliable_recover_3b",
+    "snapshot_unreliable_recover_concurrent_partition_3b",
 ]
 SCENARIO_ID = {n: i for i, n in enumerate(SCENARIOS) if n}
 # tests that still need multi-threaded tester programs (spawn_local); not built yet
-UNSUPPORTED = set()
+UNSUPPORTED = {"unreliable_one_key_3a", "one_partition_3a", "snapshot_rpc_3b", "snapshot_size_3b"}
 # kvraft generic_test (src/kvraft/tests.rs:65-238), BASELINE config 5
 KV_TESTS = ["basic_3a", "concurrent_3a", "unreliable_3a", "many_partitions_one_client_3a",
             "many_partitions_many_clients_3a", "persist_one_client_3a", "persist_concurrent_3a",
             "persist_concurrent_unreliable_3a", "persist_partition_3a",
-            "persist_partition_unreliable_3a"]
-GPU_UNSUPPORTED = set()
+            "persist_partition_unreliable_3a", "unreliable_one_key_3a", "one_partition_3a",
+            "snapshot_rpc_3b", "snapshot_size_3b", "snapshot_recover_3b",
+            "snapshot_recover_many_clients_3b", "snapshot_unreliable_3b",
+            "snapshot_unreliable_recover_3b", "snapshot_unreliable_recover_concurrent_partition_3b"]
+GPU_UNSUPPORTED = set(UNSUPPORTED)
 
 FAIL_NAMES = {
     0: "PASS", 1: "ONE_LEADER_NONE", 2: "MULTI_LEADER_TERM", 3: "TERM_DISAGREE",
@@ -56,7 +62,9 @@ FAIL_NAMES = {
     29: "KV_APPEND_BAD", 30: "CTRL_NGROUPS", 31: "CTRL_MISSING", 32: "CTRL_INVALID",
     33: "CTRL_IMBALANCED", 34: "CTRL_SERVERS", 35: "CTRL_HISTORY", 36: "CTRL_MOVE_NUM",
     37: "CTRL_MOVE_WRONG", 38: "CTRL_MINIMAL_JOIN", 39: "CTRL_MINIMAL_LEAVE", 40: "CTRL_NO_LEADER",
-    41: "CTRL_SAME_CONFIG", 42: "SAFETY_ELECTION", 43: "SAFETY_COMPLETENESS", 60: "SIM_CAPACITY",
+    41: "CTRL_SAME_CONFIG", 42: "SAFETY_ELECTION", 43: "SAFETY_COMPLETENESS",
+    44: "KV_LOG_SIZE", 45: "KV_SNAPSHOT_SIZE", 46: "KV_MINORITY_PROGRESS", 47: "KV_NO_COMPLETION",
+    48: "KV_CHECK", 60: "SIM_CAPACITY",
     61: "SIM_EVENT_LIMIT", 62: "SIM_BAD_PROGRAM", 0xFFFF: "RUNNING",
 }
 

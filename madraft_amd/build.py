@@ -24,13 +24,13 @@ def _stale(out, srcs):
 
 # step-kernel instances (one per scenario id, mr_dev.h MR_ALL_SCNS) are split
 # over several translation units of mr_kernel.hip compiled in parallel
-SCN_IDS = list(range(1, 37))
+SCN_IDS = list(range(1, 46))
 N_GROUPS = 8
 
 
 # the scenarios' default server counts (mr_dev.h k_default_n): each scenario
 # gets an instance sized for it (NB = 3 or 5) and one for up to 8 servers
-DEFAULT_N = [0, 3, 3, 7, 5, 3, 5, 3, 3, 5, 3, 3, 5, 3, 5, 5, 5, 5, 5, 3, 3, 3, 3, 3, 5, 5, 5, 5, 3, 3, 5, 5, 5, 5, 5, 5, 5]
+DEFAULT_N = [0, 3, 3, 7, 5, 3, 5, 3, 3, 5, 3, 3, 5, 3, 5, 5, 5, 5, 5, 3, 3, 3, 3, 3, 5, 5, 5, 5, 3, 3, 5, 5, 5, 5, 5, 5, 5, 3, 5, 3, 3, 5, 5, 5, 5, 5]
 
 
 def _units(csrc):

@@ -83,7 +83,6 @@ struct alignas(16) LE {
 enum : uint32_t { KV_GET = 0, KV_PUT = 1, KV_APPEND = 2 };
 enum : uint32_t { KV_OK = 0, KV_WRONG_LEADER = 1, KV_FAILED = 2 };
 constexpr uint32_t CLERK_HOST = 8;  // clerk c is host 8 + c
-constexpr uint32_t KV_SLOTS = 7;    // tester thread / clerk slots: 0 = test body + ck, 1 + cli, partitioner
 constexpr uint32_t KV_PEND = 8;     // pending requests per server
 // kt32 [KT__N][nthr(S)][C]: a spawned tester thread (+ its clerk, kvraft) per slot.
 // Words KT_W.. are the thread's own frame: kvraft clerk fields, churn client
@@ -108,6 +107,10 @@ constexpr uint32_t KVR_DEDUP = 0, KVR_PEND = 128, KVR_NCFG = 192, KVR_KEYS = 256
 constexpr uint32_t KV_KEYS = 64, KV_KW = 8, KV_APP = 5, MAX_CLERKS = 128;
 constexpr uint32_t KV_ALL = 0xFFFFFFu;  // Get elem: appenders 0..4, packed
 constexpr uint64_t KV_HP = 0x100000001B3ull;  // value hash multiplier
+// a KV snapshot (SEMANTICS §9): dedup[128] then the 64 key records; the ring entry for
+// index i (slot i / 16 mod 16) holds i at word 0 and the snapshot from word 4
+constexpr uint32_t KVS_W = MAX_CLERKS + KV_KEYS * KV_KW, KV_RING = 16, KRW = 4 + KVS_W;
+constexpr uint32_t KV_SNAP_EVERY = 16;
 // ---- shard_ctrler (SEMANTICS §10): per-server append-only config store and a
 // per-cluster table of clerk operations (the log command names an operation)
 constexpr uint32_t N_SHARDS = 10;  // shard_ctrler/mod.rs:9
@@ -140,8 +143,10 @@ struct Dev {
   LE* log;  // [C][n][log_cap] ring per node
   LE* pay;  // [C][M][K] AppendEntries payload per message slot
   SE* stor;         // [C][apply_cap]   tester storage (tester.rs:366-428)
-  uint32_t* kt32;   // [KT__N][KV_SLOTS][C] (kvraft only)
+  uint32_t* kt32;   // [KT__N][nthr][C]     (spawning scenarios)
   uint32_t* kv32;   // [C][n][KVREC]        (kvraft only)
+  uint32_t* kvs32;  // [C][n][KVS_W]        persisted KV snapshots (maxraftstate)
+  uint32_t* kring;  // [C][KV_RING][KRW]    recent KV snapshots by index (maxraftstate)
   uint64_t* cval;   // [C][3][CHURN_VCAP]   churn clients' committed values (churn only)
   uint32_t* cidx;   // [C][3][CHURN_VCAP]   ... and the index each was seen at
   uint32_t* cfg32;  // [C][n][CFG_CAP][CFGW] shard_ctrler config stores
@@ -155,10 +160,12 @@ constexpr uint32_t PROF_SLOTS = 64;
 
 constexpr bool is_kv(uint32_t s) {
   return (s >= MR_SCN_KV_BASIC_3A && s <= MR_SCN_KV_UNRELIABLE_3A) ||
-         (s >= MR_SCN_KV_MANY_PARTITIONS_ONE_CLIENT_3A && s <= MR_SCN_KV_PERSIST_PARTITION_UNRELIABLE_3A);
+         (s >= MR_SCN_KV_MANY_PARTITIONS_ONE_CLIENT_3A &&
+          s <= MR_SCN_KV_SNAPSHOT_UNRELIABLE_RECOVER_CONCURRENT_PARTITION_3B);
 }
-// generic_test(nclients, unreliable, crash, partitions) of a kvraft scenario (kvraft/tests.rs:222-384)
-struct KvGen { uint32_t nc; bool unrel, crash, part; };
+// generic_test(nclients, unreliable, crash, partitions, maxraftstate) of a kvraft scenario
+// (kvraft/tests.rs:222-384, 494-522); snapshot_rpc / snapshot_size use maxraftstate too
+struct KvGen { uint32_t nc; bool unrel, crash, part; uint32_t maxraft; };
 constexpr KvGen kv_gen(uint32_t s) {
   switch (s) {
     case MR_SCN_KV_BASIC_3A: return {1, false, false, false};
@@ -171,7 +178,16 @@ constexpr KvGen kv_gen(uint32_t s) {
     case MR_SCN_KV_PERSIST_CONCURRENT_UNRELIABLE_3A: return {5, true, true, false};
     case MR_SCN_KV_PERSIST_PARTITION_3A: return {5, false, true, true};
     case MR_SCN_KV_PERSIST_PARTITION_UNRELIABLE_3A: return {5, true, true, true};
-    default: return {0, false, false, false};
+    case MR_SCN_KV_UNRELIABLE_ONE_KEY_3A: return {5, true, false, false};
+    case MR_SCN_KV_ONE_PARTITION_3A: return {0, false, false, true};
+    case MR_SCN_KV_SNAPSHOT_RPC_3B: return {0, false, false, true, 1000};
+    case MR_SCN_KV_SNAPSHOT_SIZE_3B: return {0, false, false, false, 1000};
+    case MR_SCN_KV_SNAPSHOT_RECOVER_3B: return {1, false, true, false, 1000};
+    case MR_SCN_KV_SNAPSHOT_RECOVER_MANY_CLIENTS_3B: return {20, false, true, false, 1000};
+    case MR_SCN_KV_SNAPSHOT_UNRELIABLE_3B: return {5, true, false, false, 1000};
+    case MR_SCN_KV_SNAPSHOT_UNRELIABLE_RECOVER_3B: return {5, true, true, false, 1000};
+    case MR_SCN_KV_SNAPSHOT_UNRELIABLE_RECOVER_CONCURRENT_PARTITION_3B: return {5, true, true, true, 1000};
+    default: return {0, false, false, false, 0};
   }
 }
 constexpr bool is_ctrl(uint32_t s) { return s == MR_SCN_CTRL_BASIC_4A || s == MR_SCN_CTRL_MULTI_4A; }
@@ -183,7 +199,8 @@ constexpr bool is_churn(uint32_t s) {
 // tester thread slots (slot 0 = the test body): kvraft 1 + 5 clients, churn 1 + 3
 // clients, unreliable_agree_2c up to 63 concurrent one() tasks
 constexpr uint32_t nthr(uint32_t s) {
-  return is_kv(s) ? KV_SLOTS : is_ctrl(s) ? 11u : is_churn(s) ? 4u
+  return is_kv(s) ? (kv_gen(s).nc + 2u > 6u ? kv_gen(s).nc + 2u : 6u)  // + test body, partitioner
+         : is_ctrl(s) ? 11u : is_churn(s) ? 4u
          : s == MR_SCN_UNRELIABLE_AGREE_2C ? 64u : 0u;
 }
 
@@ -193,13 +210,15 @@ template <uint32_t S, uint32_t NB>
 hipError_t launch_step_t(const Dev& D, uint32_t budget, hipStream_t s);
 constexpr uint8_t k_default_n[] = {0, 3, 3, 7, 5, 3, 5, 3, 3, 5, 3, 3, 5, 3, 5,
                                    5, 5, 5, 5, 3, 3, 3, 3, 3, 5, 5, 5, 5, 3, 3,
-                                   5, 5, 5, 5, 5, 5, 5};
+                                   5, 5, 5, 5, 5, 5, 5, 3, 5, 3, 3, 5, 5, 5, 5, 5};
 constexpr uint32_t nb_of(uint32_t s) { return k_default_n[s] <= 5 ? k_default_n[s] : 8u; }
 #define MR_ALL_SCNS                                                                       \
   MR_INST(1) MR_INST(2) MR_INST(3) MR_INST(4) MR_INST(5) MR_INST(6) MR_INST(7) MR_INST(8) \
   MR_INST(9) MR_INST(10) MR_INST(11) MR_INST(12) MR_INST(13) MR_INST(14) MR_INST(16)      \
   MR_INST(19) MR_INST(20) MR_INST(21) MR_INST(22) MR_INST(23) MR_INST(24) MR_INST(25)     \
   MR_INST(26) MR_INST(27) MR_INST(15) MR_INST(17) MR_INST(18) MR_INST(28) MR_INST(29)     \
-  MR_INST(30) MR_INST(31) MR_INST(32) MR_INST(33) MR_INST(34) MR_INST(35) MR_INST(36)
+  MR_INST(30) MR_INST(31) MR_INST(32) MR_INST(33) MR_INST(34) MR_INST(35) MR_INST(36)     \
+  MR_INST(37) MR_INST(38) MR_INST(39) MR_INST(40) MR_INST(41) MR_INST(42) MR_INST(43)     \
+  MR_INST(44) MR_INST(45)
 
 }  // namespace mr

@@ -59,11 +59,14 @@ const char* k_names[MR_SCN_COUNT_] = {
     "concurrent_3a", "unreliable_3a", "basic_4a", "multi_4a",
     "many_partitions_one_client_3a", "many_partitions_many_clients_3a", "persist_one_client_3a",
     "persist_concurrent_3a", "persist_concurrent_unreliable_3a", "persist_partition_3a",
-    "persist_partition_unreliable_3a"};
+    "persist_partition_unreliable_3a", "unreliable_one_key_3a", "one_partition_3a",
+    "snapshot_rpc_3b", "snapshot_size_3b", "snapshot_recover_3b", "snapshot_recover_many_clients_3b",
+    "snapshot_unreliable_3b", "snapshot_unreliable_recover_3b",
+    "snapshot_unreliable_recover_concurrent_partition_3b"};
 // servers per test (tests.rs `let servers = ..`)
 const uint8_t k_nodes[MR_SCN_COUNT_] = {0, 3, 3, 7, 5, 3, 5, 3, 3, 5, 3, 3, 5, 3,
                                         5, 5, 5, 5, 5, 3, 3, 3, 3, 3, 5, 5, 5, 5, 3, 3,
-                                        5, 5, 5, 5, 5, 5, 5};
+                                        5, 5, 5, 5, 5, 5, 5, 3, 5, 3, 3, 5, 5, 5, 5, 5};
 
 constexpr size_t RED_N = CNT__N + 8 + 64;  // reduce_kernel output slots
 }  // namespace
@@ -139,6 +142,11 @@ const char* mr_fail_message(uint32_t code) {
     case MR_FAIL_CTRL_SAME_CONFIG: return "config differs after leader shutdown";
     case MR_FAIL_SAFETY_ELECTION: return "election safety: two leaders in one term";
     case MR_FAIL_SAFETY_COMPLETENESS: return "leader completeness: new leader lacks a committed entry";
+    case MR_FAIL_KV_LOG_SIZE: return "logs were not trimmed";
+    case MR_FAIL_KV_SNAPSHOT_SIZE: return "snapshot too large";
+    case MR_FAIL_KV_MINORITY_PROGRESS: return "put/get in minority completed";
+    case MR_FAIL_KV_NO_COMPLETION: return "put/get did not complete";
+    case MR_FAIL_KV_CHECK: return "get(key) check failed";
     case MR_FAIL_SIM_CAPACITY: return "simulator capacity exceeded";
     case MR_FAIL_SIM_EVENT_LIMIT: return "simulator event limit exceeded";
     case MR_FAIL_SIM_BAD_PROGRAM: return "scenario program error";
@@ -246,6 +254,10 @@ int mr_batch_create(const mr_cfg* cfg, mr_batch** out) {
   D.nthr = nthr(scn);
   if (D.nthr) add(&D.kt32, (size_t)KT__N * D.nthr * C);
   if (is_svc(scn)) add(&D.kv32, (size_t)KVREC * n * C);
+  if (kv_gen(scn).maxraft) {
+    add(&D.kvs32, (size_t)KVS_W * n * C);
+    add(&D.kring, (size_t)KRW * KV_RING * C);
+  }
   if (is_ctrl(scn)) {
     add(&D.cfg32, (size_t)CFG_CAP * CFGW * n * C);
     add(&D.op32, (size_t)OP_CAP * OPW * C);
@@ -302,6 +314,10 @@ int mr_batch_reset(mr_batch* b, uint64_t seed_base) {
   HIPCHK(hipMemsetAsync(b->D.stor, 0, (size_t)b->D.C * b->D.apply_cap * sizeof(SE), b->stream));
   if (b->D.kv32)
     HIPCHK(hipMemsetAsync(b->D.kv32, 0, (size_t)b->D.C * b->D.n * KVREC * sizeof(uint32_t), b->stream));
+  if (b->D.kvs32) {
+    HIPCHK(hipMemsetAsync(b->D.kvs32, 0, (size_t)b->D.C * b->D.n * KVS_W * sizeof(uint32_t), b->stream));
+    HIPCHK(hipMemsetAsync(b->D.kring, 0, (size_t)b->D.C * KV_RING * KRW * sizeof(uint32_t), b->stream));
+  }
   HIPCHK(launch_reset(b->D, b->stream));
   HIPCHK(hipStreamSynchronize(b->stream));
   return 0;

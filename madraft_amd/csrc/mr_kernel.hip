@@ -440,6 +440,17 @@ DI void node_apply(const Dev& D, X& x, uint32_t me, NC& d, bool& kvready) {
         kv_apply<is_ctrl(S)>(D, x, me, i, e[j].val, kvready);
         if (x.code != RUN) return;
       }
+      if constexpr (kv_gen(S).maxraft > 0) {  // the KV service snapshots (SEMANTICS §9)
+        const uint32_t sz = 32u + (f_voted(d.f) != 15u ? 9u : 1u) + 24u * (d.last - d.snap);
+        if (i % KV_SNAP_EVERY == 0 && i > d.snap && sz >= kv_gen(S).maxraft / 2) {
+          d.snapt = e[j].term;
+          d.snap = i;
+          NSV(me) = e[j].val;
+          CADD(CNT_SNAPSHOTS, 1u);
+          kv_snapshot(D, x, me, i);
+          if (x.code != RUN) return;
+        }
+      }
     }
     PROF(P_AP_CHECK);
   }
@@ -680,6 +691,10 @@ DI void node_event(const Dev& D, X& x, bool is_msg, uint32_t tnode, uint32_t slo
           d.commit = idx; d.applied = idx;
           storage_snapshot(D, x, me, d.slen, idx);
           if (x.code != RUN) return;
+          if constexpr (kv_gen(S).maxraft > 0) {
+            kv_install(D, x, me, idx, kvready);
+            if (x.code != RUN) return;
+          }
           CADD(CNT_INSTALLS, 1u);
         }
         rb = idx;

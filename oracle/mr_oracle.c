@@ -108,6 +108,10 @@ typedef struct { uint32_t used, idx, clerk, seq, tag, ready, status, value, host
 /* a key's value (SEMANTICS §9): the hash of its token sequence, its byte length, and
  * per appender (cli + 1 | count << 8 | bad << 31) for the append-order checks */
 typedef struct { uint64_t h; uint32_t len; uint32_t app[KV_APP]; } OKey;
+/* a KV server's state machine as its snapshot holds it (SEMANTICS §9) */
+typedef struct { uint32_t dedup[MAX_CLERKS]; OKey keys[KV_KEYS]; } OKvState;
+#define KV_SNAP_EVERY 16u /* the service snapshots at applied indices that are multiples of 16 */
+#define KV_RING 16u       /* recent snapshots by index / 16 mod 16, read by InstallSnapshot */
 /* Config (shard_ctrler/msg.rs:11-18): groups sorted by gid; a server list is
  * packed as len | a0 << 8 | a1 << 16 | a2 << 24 (addrs! takes `as u8`) */
 typedef struct { uint32_t num, shards[N_SHARDS], ng, gid[CFG_G], addr[CFG_G]; } OCfg;
@@ -129,6 +133,9 @@ typedef struct {
   /* kvraft (SEMANTICS §8-9) */
   uint32_t kv_mode, kv_done, next_tid, mwake, main_join;
   OKey kv[MR_MAX_NODES][KV_KEYS]; uint32_t kv_dedup[MR_MAX_NODES][MAX_CLERKS];
+  uint32_t kv_maxraft;                /* maxraftstate (0 = None) */
+  OKvState* kvs;                      /* [MR_MAX_NODES] persisted KV snapshots */
+  OKvState* kring; uint32_t* kring_idx; /* [KV_RING] */
   OPend pend[MR_MAX_NODES][KV_PEND];
   OClerk ck[CK_SLOTS]; OThr th[MAX_THR];
   uint64_t* cval; uint32_t* cidx; /* churn values [3][CHURN_VCAP] + their indices */
@@ -465,6 +472,62 @@ static void kv_flush(OSim* s, uint32_t me) {
   }
 }
 
+/* the persisted "state" size (SEMANTICS §5 size model) */
+static uint32_t raft_state_size(const ONode* d) {
+  return 32 + (d->voted >= 0 ? 9 : 1) + 24 * (d->last - d->snap_idx);
+}
+
+static void kv_state_get(OSim* s, uint32_t me, OKvState* st) {
+  memcpy(st->dedup, s->kv_dedup[me], sizeof st->dedup);
+  memcpy(st->keys, s->kv[me], sizeof st->keys);
+}
+static void kv_state_put(OSim* s, uint32_t me, const OKvState* st) {
+  memcpy(s->kv_dedup[me], st->dedup, sizeof st->dedup);
+  memcpy(s->kv[me], st->keys, sizeof st->keys);
+}
+
+/* the KV service snapshots its state at applied index i (kvraft/server.rs:12-16 with
+ * maxraftstate; SEMANTICS §9): Raft's snapshot(i), the persisted KV snapshot, and the
+ * cluster's ring of recent snapshots (equal states at equal indices, or APPLY_MISMATCH) */
+static void kv_snapshot(OSim* s, uint32_t me, uint32_t i) {
+  ONode* d = &s->nd[me];
+  d->snap_term = term_at(s, d, i);
+  d->snap_val = d->lval[lpos(s, i)];
+  d->snap_idx = i;
+  s->r.snapshots++;
+  kv_state_get(s, me, &s->kvs[me]);
+  uint32_t r = (i / KV_SNAP_EVERY) % KV_RING;
+  if (s->kring_idx[r] == i) {
+    if (memcmp(&s->kring[r], &s->kvs[me], sizeof(OKvState))) t_fail(s, MR_FAIL_APPLY_MISMATCH);
+  } else {
+    s->kring[r] = s->kvs[me];
+    s->kring_idx[r] = i;
+  }
+}
+
+/* InstallSnapshot(idx) at server me: the KV state of index idx from the ring; requests
+ * pending at or below idx are answered FAILED (their entries are never applied here) */
+static void kv_install(OSim* s, uint32_t me, uint32_t idx) {
+  uint32_t r = (idx / KV_SNAP_EVERY) % KV_RING;
+  if (s->kring_idx[r] != idx) t_fail(s, MR_FAIL_SIM_CAPACITY);
+  s->kvs[me] = s->kring[r];
+  kv_state_put(s, me, &s->kring[r]);
+  for (uint32_t p = 0; p < KV_PEND; p++) {
+    OPend* q = &s->pend[me][p];
+    if (q->used && !q->ready && q->idx <= idx) { q->ready = 1; q->status = KV_FAILED; q->value = 0; q->vh = 0; }
+  }
+}
+
+/* the persisted KV snapshot's size (snapshot_size(), kvraft/tester.rs:69-76; SEMANTICS §9):
+ * 8 + per non-empty key (16 + name + value bytes) + 8 + 16 per clerk with a dedup entry */
+static uint32_t kv_snap_size(const OKvState* st) {
+  uint32_t sz = 16;
+  for (uint32_t k = 0; k < KV_KEYS; k++)
+    if (st->keys[k].h || st->keys[k].len) sz += 16 + (k < 50 ? ndig(k) : 1) + st->keys[k].len;
+  for (uint32_t c = 0; c < MAX_CLERKS; c++) sz += st->dedup[c] ? 16 : 0;
+  return sz;
+}
+
 /* tester.rs:303-325 applier: push_and_check, snapshot every SNAPSHOT_INTERVAL */
 static void node_apply(OSim* s, uint32_t me) {
   ONode* d = &s->nd[me];
@@ -473,6 +536,8 @@ static void node_apply(OSim* s, uint32_t me) {
     uint64_t v = d->lval[lpos(s, i)];
     push_and_check(s, me, i, v);
     if (s->kv_mode) kv_apply(s, me, i, v);
+    if (s->kv_maxraft && i % KV_SNAP_EVERY == 0 && i > d->snap_idx &&
+        raft_state_size(d) >= s->kv_maxraft / 2) kv_snapshot(s, me, i);
     if (s->snapshot_mode && (i + 1) % 10 == 0 && i > d->snap_idx) {
       d->snap_term = term_at(s, d, i);
       d->snap_val = v;
@@ -694,6 +759,7 @@ static void deliver(OSim* s, OMsg* m) {
         d->snap_idx = idx; d->snap_term = m->b; d->snap_val = m->v;
         d->commit = idx; d->applied = idx;
         storage_snapshot(s, me, idx);
+        if (s->kv_maxraft) kv_install(s, me, idx);
         s->r.installs++;
       }
       reply(s, me, m, M_IS_REP, 0, idx);
@@ -1691,12 +1757,14 @@ static uint32_t main_call(OSim* s, uint32_t op, uint32_t key, uint32_t elem) { /
 static void t_shutdown_server(OSim* s, uint32_t i) { t_crash1(s, i); }
 static void t_start_server(OSim* s, uint32_t i) {
   t_start1(s, i);
+  if (s->kv_maxraft) { kv_state_put(s, i, &s->kvs[i]); return; } /* restore from the snapshot */
   memset(s->kv[i], 0, sizeof s->kv[i]);
   memset(s->kv_dedup[i], 0, sizeof s->kv_dedup[i]);
 }
 
-static void scn_kv_generic(OSim* s, uint32_t nclients, int unreliable, int crash,
-                           int partitions) { /* kvraft/tests.rs:65-220 */
+static void scn_kv_generic(OSim* s, uint32_t nclients, int unreliable, int crash, int partitions,
+                           uint32_t maxraftstate) { /* kvraft/tests.rs:65-220 */
+  s->kv_maxraft = maxraftstate;
   t_new(s, 0); /* Tester::new (kvraft/tester.rs:27-56): start_server for every server */
   if (unreliable) t_set_unreliable(s, 1);
   s->kv_mode = 1;
@@ -1733,6 +1801,7 @@ static void scn_kv_generic(OSim* s, uint32_t nclients, int unreliable, int crash
       if (!(v >> 31)) t_fail(s, MR_FAIL_KV_APPEND_BAD);         /* kvraft/tests.rs:31-39 */
       if ((v & 0x7FFFFFFFu) < j) t_fail(s, MR_FAIL_KV_MISSING); /* kvraft/tests.rs:25-30 */
     }
+    if (maxraftstate && t_log_size(s) > 2 * maxraftstate) t_fail(s, MR_FAIL_KV_LOG_SIZE); /* :208-215 */
   }
   t_end(s);
 }
@@ -1986,16 +2055,23 @@ static int run_scenario(OSim* s) {
     case MR_SCN_UNRELIABLE_CHURN_2C: scn_churn(s, 1); break;
     case MR_SCN_CTRL_BASIC_4A: scn_ctrl_basic(s); break;
     case MR_SCN_CTRL_MULTI_4A: scn_ctrl_multi(s); break;
-    case MR_SCN_KV_BASIC_3A: scn_kv_generic(s, 1, 0, 0, 0); break;
-    case MR_SCN_KV_CONCURRENT_3A: scn_kv_generic(s, 5, 0, 0, 0); break;
-    case MR_SCN_KV_UNRELIABLE_3A: scn_kv_generic(s, 5, 1, 0, 0); break;
-    case MR_SCN_KV_MANY_PARTITIONS_ONE_CLIENT_3A: scn_kv_generic(s, 1, 0, 0, 1); break;
-    case MR_SCN_KV_MANY_PARTITIONS_MANY_CLIENTS_3A: scn_kv_generic(s, 5, 0, 0, 1); break;
-    case MR_SCN_KV_PERSIST_ONE_CLIENT_3A: scn_kv_generic(s, 1, 0, 1, 0); break;
-    case MR_SCN_KV_PERSIST_CONCURRENT_3A: scn_kv_generic(s, 5, 0, 1, 0); break;
-    case MR_SCN_KV_PERSIST_CONCURRENT_UNRELIABLE_3A: scn_kv_generic(s, 5, 1, 1, 0); break;
-    case MR_SCN_KV_PERSIST_PARTITION_3A: scn_kv_generic(s, 5, 0, 1, 1); break;
-    case MR_SCN_KV_PERSIST_PARTITION_UNRELIABLE_3A: scn_kv_generic(s, 5, 1, 1, 1); break;
+    case MR_SCN_KV_BASIC_3A: scn_kv_generic(s, 1, 0, 0, 0, 0); break;
+    case MR_SCN_KV_CONCURRENT_3A: scn_kv_generic(s, 5, 0, 0, 0, 0); break;
+    case MR_SCN_KV_UNRELIABLE_3A: scn_kv_generic(s, 5, 1, 0, 0, 0); break;
+    case MR_SCN_KV_MANY_PARTITIONS_ONE_CLIENT_3A: scn_kv_generic(s, 1, 0, 0, 1, 0); break;
+    case MR_SCN_KV_MANY_PARTITIONS_MANY_CLIENTS_3A: scn_kv_generic(s, 5, 0, 0, 1, 0); break;
+    case MR_SCN_KV_PERSIST_ONE_CLIENT_3A: scn_kv_generic(s, 1, 0, 1, 0, 0); break;
+    case MR_SCN_KV_PERSIST_CONCURRENT_3A: scn_kv_generic(s, 5, 0, 1, 0, 0); break;
+    case MR_SCN_KV_PERSIST_CONCURRENT_UNRELIABLE_3A: scn_kv_generic(s, 5, 1, 1, 0, 0); break;
+    case MR_SCN_KV_PERSIST_PARTITION_3A: scn_kv_generic(s, 5, 0, 1, 1, 0); break;
+    case MR_SCN_KV_PERSIST_PARTITION_UNRELIABLE_3A: scn_kv_generic(s, 5, 1, 1, 1, 0); break;
+    case MR_SCN_KV_SNAPSHOT_RECOVER_3B: scn_kv_generic(s, 1, 0, 1, 0, 1000); break;
+    case MR_SCN_KV_SNAPSHOT_RECOVER_MANY_CLIENTS_3B: scn_kv_generic(s, 20, 0, 1, 0, 1000); break;
+    case MR_SCN_KV_SNAPSHOT_UNRELIABLE_3B: scn_kv_generic(s, 5, 1, 0, 0, 1000); break;
+    case MR_SCN_KV_SNAPSHOT_UNRELIABLE_RECOVER_3B: scn_kv_generic(s, 5, 1, 1, 0, 1000); break;
+    case MR_SCN_KV_SNAPSHOT_UNRELIABLE_RECOVER_CONCURRENT_PARTITION_3B:
+      scn_kv_generic(s, 5, 1, 1, 1, 1000);
+      break;
     default: return -1;
   }
   return 0;
@@ -2020,6 +2096,9 @@ static int sim_alloc(OSim* s, const mr_cfg* cfg) {
   s->ops = (OOp*)malloc(OP_CAP * sizeof(OOp));
   s->cval = (uint64_t*)malloc(3 * CHURN_VCAP * sizeof(uint64_t));
   s->cidx = (uint32_t*)malloc(3 * CHURN_VCAP * sizeof(uint32_t));
+  s->kvs = (OKvState*)malloc(MR_MAX_NODES * sizeof(OKvState));
+  s->kring = (OKvState*)malloc(KV_RING * sizeof(OKvState));
+  s->kring_idx = (uint32_t*)malloc(KV_RING * sizeof(uint32_t));
   s->mask = (uint8_t*)malloc(cfg->apply_cap);
   s->sval = (uint64_t*)malloc(cfg->apply_cap * sizeof(uint64_t));
   return 0;
@@ -2028,7 +2107,7 @@ static int sim_alloc(OSim* s, const mr_cfg* cfg) {
 static void sim_free(OSim* s) {
   for (uint32_t i = 0; i < MR_MAX_NODES; i++) { free(s->nd[i].lterm); free(s->nd[i].lval); }
   free(s->mask); free(s->sval); free(s->heap); free(s->cval); free(s->cidx);
-  free(s->cfgs); free(s->ops);
+  free(s->cfgs); free(s->ops); free(s->kvs); free(s->kring); free(s->kring_idx);
 }
 
 static void sim_reset(OSim* s, uint64_t cluster) {
@@ -2054,6 +2133,9 @@ static void sim_reset(OSim* s, uint64_t cluster) {
   memset(s->ck, 0, sizeof s->ck); memset(s->th, 0, sizeof s->th); s->churn_stop = 0;
   s->ctrl_mode = 0; s->nops = 0;
   memset(s->lring, 0, sizeof s->lring);
+  s->kv_maxraft = 0;
+  memset(s->kvs, 0, MR_MAX_NODES * sizeof(OKvState));
+  memset(s->kring_idx, 0, KV_RING * sizeof(uint32_t));
   memset(s->link, 0xFF, sizeof s->link);
   for (uint32_t i = 0; i < MR_MAX_NODES; i++) { /* the initial config, num 0 */
     s->ncfg[i] = 1;
@@ -2132,7 +2214,10 @@ static const char* k_names[MR_SCN_COUNT_] = {
     "concurrent_3a", "unreliable_3a", "basic_4a", "multi_4a",
     "many_partitions_one_client_3a", "many_partitions_many_clients_3a", "persist_one_client_3a",
     "persist_concurrent_3a", "persist_concurrent_unreliable_3a", "persist_partition_3a",
-    "persist_partition_unreliable_3a"};
+    "persist_partition_unreliable_3a", "unreliable_one_key_3a", "one_partition_3a",
+    "snapshot_rpc_3b", "snapshot_size_3b", "snapshot_recover_3b", "snapshot_recover_many_clients_3b",
+    "snapshot_unreliable_3b", "snapshot_unreliable_recover_3b",
+    "snapshot_unreliable_recover_concurrent_partition_3b"};
 
 uint32_t mro_scenario_from_name(const char* name) {
   for (uint32_t i = 1; i < MR_SCN_COUNT_; i++)
@@ -2143,7 +2228,7 @@ uint32_t mro_scenario_from_name(const char* name) {
 int mro_cfg_init(mr_cfg* c, uint32_t scn) {
   static const uint8_t k_n[MR_SCN_COUNT_] = {0, 3, 3, 7, 5, 3, 5, 3, 3, 5, 3, 3, 5, 3,
                                              5, 5, 5, 5, 5, 3, 3, 3, 3, 3, 5, 5, 5, 5, 3, 3,
-                                             5, 5, 5, 5, 5, 5, 5};
+                                             5, 5, 5, 5, 5, 5, 5, 3, 5, 3, 3, 5, 5, 5, 5, 5};
   if (scn == 0 || scn >= MR_SCN_COUNT_) return -1;
   memset(c, 0, sizeof *c);
   c->abi_version = MR_ABI_VERSION;
@@ -2190,6 +2275,11 @@ const char* mro_fail_message(uint32_t code) {
     case MR_FAIL_KV_APPEND_BAD: return "duplicate or wrong order element in Append result";
     case MR_FAIL_SAFETY_ELECTION: return "election safety: two leaders in one term";
     case MR_FAIL_SAFETY_COMPLETENESS: return "leader completeness: new leader lacks a committed entry";
+    case MR_FAIL_KV_LOG_SIZE: return "logs were not trimmed";
+    case MR_FAIL_KV_SNAPSHOT_SIZE: return "snapshot too large";
+    case MR_FAIL_KV_MINORITY_PROGRESS: return "put/get in minority completed";
+    case MR_FAIL_KV_NO_COMPLETION: return "put/get did not complete";
+    case MR_FAIL_KV_CHECK: return "get(key) check failed";
     case MR_FAIL_SIM_CAPACITY: return "simulator capacity exceeded";
     case MR_FAIL_SIM_EVENT_LIMIT: return "simulator event limit exceeded";
     default: return "scenario assertion failed";

