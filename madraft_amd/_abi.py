@@ -40,7 +40,7 @@ SCENARIOS = [
 ]
 SCENARIO_ID = {n: i for i, n in enumerate(SCENARIOS) if n}
 # tests that still need multi-threaded tester programs (spawn_local); not built yet
-UNSUPPORTED = {"unreliable_one_key_3a", "one_partition_3a", "snapshot_rpc_3b", "snapshot_size_3b"}
+UNSUPPORTED = set()
 # kvraft generic_test (src/kvraft/tests.rs:65-238), BASELINE config 5
 KV_TESTS = ["basic_3a", "concurrent_3a", "unreliable_3a", "many_partitions_one_client_3a",
             "many_partitions_many_clients_3a", "persist_one_client_3a", "persist_concurrent_3a",

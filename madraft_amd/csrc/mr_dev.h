@@ -51,6 +51,8 @@ enum : uint32_t {
   CS_LRING_END = CS_LRING + 32,
   CS_CUT,    // server links cut (disconnect2): bit 8 (i mod 4) + j of word CS_CUT + i / 4
   CS_CUT_END = CS_CUT + 2,
+  CS_CCUT,   // clerk links cut: bit 8 (k mod 4) + j of word CS_CCUT + k / 4 = clerk host 8 + k !~ server j
+  CS_CCUT_END = CS_CCUT + 6,
   CS__N
 };
 // cs64 [C64__N][C]: per-cluster u64 scalars
@@ -94,10 +96,18 @@ enum : uint32_t {
   KT_PERM,
   KT_RVH0, KT_RVH1,  // the reply's value hash
   KT_HL0, KT_HL1,    // generic_test client: hash of its predicted value `last`
+  KT_OWN,            // the thread the clerk's calls wake (0 = the test body)
+  KT_MCL,            // 1 = a clerk of the test body in a slot that is not a thread
+  KT_TOP, KT_TKEY, KT_TELEM, KT_TCNT,  // a task's call: op, key, elem (or appender), calls
   KT__N
 };
 constexpr uint32_t KT_W = KT_ID;
 constexpr uint32_t JOIN_ALL = 0xFFFFFFFEu;
+constexpr uint32_t JOIN_ANY = 0xFFFFFFFDu;  // select! over spawned tasks: the first finish wakes
+// kvraft key ids / Put value tokens of the test bodies (SEMANTICS §9)
+constexpr uint32_t key_letter(char c) { return 50u + (uint32_t)(c - 'a'); }
+constexpr uint32_t tok_num(uint32_t v) { return v + 1u; }
+constexpr uint32_t tok_letter(char c) { return (1u << 20) + (uint32_t)(c - 'A'); }
 constexpr uint32_t CHURN_VCAP = 512;  // values one churn client may record (tests.rs:763-797)
 // kv32 [C][n][KVREC]: per-server KV state (SEMANTICS §9): dedup[clerk] at 0..127, pending
 // request p at 128 + 8p: {index (0 = free), clerk | ready << 8 | status << 9 | host << 16,

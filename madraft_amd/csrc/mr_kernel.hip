@@ -267,9 +267,13 @@ DI void rescan_min(const Dev& D, X& x) {
   x.mslot = bs;
 }
 
-// server-server link i~j cut by disconnect2 (kvraft partitions); clerk links stay up
+// link a~b cut by disconnect2 (kvraft partitions, connect_client)
 DI bool link_cut(const Dev& D, X& x, uint32_t a, uint32_t b) {
-  if (!D.links || a >= CLERK_HOST || b >= CLERK_HOST) return false;
+  if (!D.links || (a >= CLERK_HOST && b >= CLERK_HOST)) return false;
+  if (a >= CLERK_HOST || b >= CLERK_HOST) {  // clerk host 8 + k and server j
+    const uint32_t k = (a >= CLERK_HOST ? a : b) - CLERK_HOST, j = a >= CLERK_HOST ? b : a;
+    return (CS(CS_CCUT + (k >> 2)) >> (8u * (k & 3u) + j)) & 1u;
+  }
   return (CS(CS_CUT + (a >> 2)) >> (8u * (a & 3u) + b)) & 1u;
 }
 

@@ -53,6 +53,7 @@ enum { KV_OK = 0, KV_WRONG_LEADER = 1, KV_FAILED = 2 };
 #define CK_SLOTS 24u    /* clerk slots (thread slot k owns clerk k, host 8 + k) */
 #define MAX_THR 64u     /* tester thread slots (unreliable_agree_2c: concurrent one() tasks) */
 #define JOIN_ALL 0xFFFFFFFEu
+#define JOIN_ANY 0xFFFFFFFDu /* select! over spawned tasks: the first finish wakes the body */
 #define CHURN_VCAP 512u /* values a churn client may record (tests.rs:763-797) */
 /* shard_ctrler (SEMANTICS §10) */
 #define N_SHARDS 10u    /* shard_ctrler/mod.rs:9 */
@@ -93,6 +94,7 @@ typedef struct { uint64_t key; uint32_t ref; uint32_t gen; } HEnt;
 /* kvraft clerk (kvraft/client.rs ClerkCore) and the tester thread that owns it */
 typedef struct {
   uint32_t id, lh, seq, tag, nctr, waiting, got, rstat, rhint, rval; uint64_t rvh;
+  uint32_t owner, mcl; /* the thread its calls wake (0 = the test body); mcl: a test-body clerk */
   uint32_t op, key, elem;
 } OClerk;
 typedef struct {
@@ -142,6 +144,7 @@ typedef struct {
   uint32_t ctrl_mode, nops, ncfg[MR_MAX_NODES];
   uint32_t lring[32]; /* MR_F_SAFETY: (term << 4) | leader + 1 by term mod 32 */
   uint8_t link[MR_MAX_NODES]; /* server links (connect2/disconnect2): bit j of link[i] = i~j */
+  uint8_t ccut[CK_SLOTS];     /* clerk links cut: bit j of ccut[k] = clerk host 8 + k !~ server j */
   OCfg* cfgs; /* [MR_MAX_NODES][CFG_CAP] */
   OOp* ops;   /* [OP_CAP] */
   uint32_t churn_stop;
@@ -248,7 +251,10 @@ static int host_conn(OSim* s, uint32_t h) { return h < CLERK_HOST ? s->nd[h].con
 /* the link between two hosts (madsim connect2/disconnect2, kvraft/tester.rs:88-124):
  * server-server links are symmetric bits; clerk links are always up here */
 static int link_up(OSim* s, uint32_t a, uint32_t b) {
-  return a >= CLERK_HOST || b >= CLERK_HOST || ((s->link[a] >> b) & 1u);
+  if (a >= CLERK_HOST && b >= CLERK_HOST) return 1;
+  if (a >= CLERK_HOST) return !((s->ccut[a - CLERK_HOST] >> b) & 1u);
+  if (b >= CLERK_HOST) return !((s->ccut[b - CLERK_HOST] >> a) & 1u);
+  return (s->link[a] >> b) & 1u;
 }
 static uint32_t* host_nctr(OSim* s, uint32_t h) {
   if (h < CLERK_HOST) return &s->nd[h].n_ctr;
@@ -637,14 +643,18 @@ static void thr_wake(OSim* s, uint32_t slot, uint32_t t);
 static void clerk_deliver(OSim* s, OMsg* m) {
   uint32_t slot = m->dst - CLERK_HOST;
   OClerk* c = &s->ck[slot];
-  if (!host_conn(s, m->src)) { s->r.drop_deliver++; rec_host(s, 16, m->dst, m->seq); return; }
-  if (!s->th[slot].live || c->id != m->inc || !c->waiting || c->got || m->term != c->tag) {
+  if (!host_conn(s, m->src) || !link_up(s, m->src, m->dst)) {
+    s->r.drop_deliver++;
+    rec_host(s, 16, m->dst, m->seq);
+    return;
+  }
+  if (!(s->th[slot].live || c->mcl) || c->id != m->inc || !c->waiting || c->got || m->term != c->tag) {
     s->r.drop_stale++;
     rec_host(s, 17, m->dst, m->seq);
     return;
   }
   c->got = 1; c->rstat = m->a; c->rhint = m->b; c->rval = m->c; c->rvh = m->v;
-  thr_wake(s, slot, s->now);
+  thr_wake(s, c->owner, s->now);
   rec_host(s, M_KV_REP, m->dst, m->seq);
 }
 
@@ -793,6 +803,7 @@ static void on_timer(OSim* s, uint32_t me) {
 }
 
 static void client_step(OSim* s, uint32_t slot);
+static void kv_task_step(OSim* s, uint32_t slot);
 
 /* a thread becomes runnable at (t, 2, tid) (SEMANTICS §8); slot 0 is the test body */
 static void thr_wake(OSim* s, uint32_t slot, uint32_t t) {
@@ -1411,7 +1422,7 @@ static void clerk_send(OSim* s, uint32_t slot) { /* one call_timeout attempt, cl
   m.b = c->seq; m.c = c->elem; m.k = 0; m.v = 0;
   net_send(s, CLERK_HOST + slot, c->lh, &m);
   c->waiting = 1; c->got = 0;
-  thr_wake(s, slot, s->now + 500000u); /* Duration::from_millis(500) */
+  thr_wake(s, c->owner, s->now + 500000u); /* Duration::from_millis(500) */
 }
 
 static void clerk_begin(OSim* s, uint32_t slot, uint32_t op, uint32_t key, uint32_t elem) {
@@ -1443,7 +1454,7 @@ static int thr_bool(OSim* s, OThr* t, uint32_t p_q32) { /* rng.gen_bool on the t
 /* a tester thread finished (its segment record is written): wake a joining test body */
 static void thr_finish(OSim* s, uint32_t slot) {
   s->th[slot].live = 0;
-  if (s->main_join == slot) s->mwake = s->now;
+  if (s->main_join == slot || s->main_join == JOIN_ANY) s->mwake = s->now;
   if (s->main_join == JOIN_ALL) {
     uint32_t live = 0;
     for (uint32_t k = 1; k < MAX_THR; k++) live += s->th[k].live;
@@ -1634,6 +1645,7 @@ static void client_step(OSim* s, uint32_t slot) {
     case MR_SCN_CTRL_MULTI_4A: ctl_client_step(s, slot); break;
     default:
       if (s->th[slot].kind == 1) part_step(s, slot);
+      else if (s->th[slot].kind >= 2) kv_task_step(s, slot);
       else kv_client_step(s, slot);
       break;
   }
@@ -1733,6 +1745,7 @@ static void kv_spawn(OSim* s, uint32_t slot, uint32_t tid, uint32_t cli) { /* ta
   t->tid = tid; t->live = 1; t->cli = cli; t->gen = gen;
   memset(&s->ck[slot], 0, sizeof s->ck[slot]);
   s->ck[slot].id = tid; /* make_client order: ck = 0, then one clerk per client task */
+  s->ck[slot].owner = slot;
   thr_wake(s, slot, s->now);
 }
 
@@ -1744,12 +1757,183 @@ static void t_join(OSim* s, uint32_t slot) { /* JoinHandle.await */
   s->main_join = ~0u;
 }
 
-static uint32_t main_call(OSim* s, uint32_t op, uint32_t key, uint32_t elem) { /* ck.get etc. */
-  clerk_begin(s, 0, op, key, elem);
+/* a call by the test body through the clerk of slot k (ck = slot 0) */
+static uint32_t main_callk(OSim* s, uint32_t k, uint32_t op, uint32_t key, uint32_t elem) {
+  clerk_begin(s, k, op, key, elem);
   for (;;) {
     main_block(s);
-    if (clerk_resume(s, 0)) return s->ck[0].rval;
+    if (clerk_resume(s, k)) return s->ck[k].rval;
   }
+}
+static uint32_t main_call(OSim* s, uint32_t op, uint32_t key, uint32_t elem) { /* ck.get etc. */
+  return main_callk(s, 0, op, key, elem);
+}
+
+/* ---- kvraft tests with their own bodies (kvraft/tests.rs:240-342, 396-492) ---- */
+#define KEY_LETTER(c) (50u + (uint32_t)((c) - 'a')) /* keys "a".."n" (SEMANTICS §9) */
+#define TOK_NUM(v) ((v) + 1u)                         /* the Put token of decimal string v */
+#define TOK_LETTER(c) ((1u << 20) + (uint32_t)((c) - 'A'))
+static uint64_t put_hash(uint32_t tok) { return tok ? (tok + 1ull) * 0x9E3779B97F4A7C15ull : 0; }
+
+/* make_client(to) owned by the test body in slot k (kvraft/tester.rs:127-150) */
+static void main_clerk(OSim* s, uint32_t k, uint32_t id, uint32_t to) {
+  memset(&s->ck[k], 0, sizeof s->ck[k]);
+  s->ck[k].id = id; s->ck[k].mcl = k != 0; s->ck[k].owner = 0;
+  s->ccut[k] = (uint8_t)~to;
+}
+static void t_connect_client(OSim* s, uint32_t k, uint32_t to) { s->ccut[k] = (uint8_t)~to; }
+static void t_check(OSim* s, uint32_t k, uint32_t key, uint32_t tok) { /* Clerk::check */
+  main_callk(s, k, KV_GET, key, 0);
+  if (s->ck[k].rvh != put_hash(tok)) t_fail(s, MR_FAIL_KV_CHECK);
+}
+static uint32_t kv_leader(OSim* s) { /* Tester::leader (kvraft/tester.rs:171-182) */
+  for (uint32_t i = 0; i < s->n; i++) if (s->nd[i].alive && s->nd[i].role == R_L) return i;
+  return ~0u;
+}
+/* a one-key appender (kvraft/tests.rs:255-262) or a single-call task (:309-314) */
+static void kv_task_step(OSim* s, uint32_t slot) {
+  OThr* t = &s->th[slot];
+  if (t->pc == 1) {
+    if (!clerk_resume(s, slot)) { rec_simple(s, 2, t->tid & 0xFFu); return; }
+    t->j++;
+    t->pc = 0;
+  }
+  if (t->j < t->expected) {
+    uint32_t elem = t->kind == 2 ? (t->cli << 19) | t->j : (uint32_t)t->cmd;
+    clerk_begin(s, slot, (uint32_t)t->retry, t->index, elem);
+    t->pc = 1;
+    rec_simple(s, 2, t->tid & 0xFFu);
+    return;
+  }
+  rec_simple(s, 2, t->tid & 0xFFu);
+  thr_finish(s, slot);
+}
+/* make_client(to) whose calls a spawned task in slot k will make */
+static void task_clerk(OSim* s, uint32_t k, uint32_t id, uint32_t to) {
+  memset(&s->ck[k], 0, sizeof s->ck[k]);
+  s->ck[k].id = id; s->ck[k].owner = k;
+  s->ccut[k] = (uint8_t)~to;
+}
+/* task::spawn_local of a task over the clerk of its slot: `count` calls of op on key */
+static void kv_task_spawn(OSim* s, uint32_t slot, uint32_t tid, uint32_t kind, uint32_t cli,
+                          uint32_t op, uint32_t key, uint32_t elem, uint32_t count) {
+  thr_spawn(s, slot, tid);
+  OThr* t = &s->th[slot];
+  t->kind = kind; t->cli = cli; t->retry = op; t->index = key; t->cmd = elem; t->expected = count;
+}
+
+static void scn_kv_one_key(OSim* s) { /* unreliable_one_key_3a, kvraft/tests.rs:240-274 */
+  t_new(s, 0);
+  t_set_unreliable(s, 1);
+  s->kv_mode = 1;
+  s->th[0].live = 1;
+  main_clerk(s, 0, 0, 0xFFu);
+  const uint32_t K = KEY_LETTER('k');
+  main_call(s, KV_PUT, K, 0);
+  for (uint32_t i = 0; i < 5; i++) { /* make_client(&t.all()), then spawn its appender */
+    task_clerk(s, 1 + i, 1 + i, 0xFFu);
+    kv_task_spawn(s, 1 + i, 1 + i, 2, i, KV_APPEND, K, 0, 10);
+  }
+  t_join_all(s);
+  uint32_t v = main_call(s, KV_GET, K, KV_ALL);
+  for (uint32_t i = 0; i < 5; i++) { /* check_concurrent_appends(&vx, &counts) */
+    uint32_t f = (v >> (6 * i)) & 63u;
+    if (!(f >> 5)) t_fail(s, MR_FAIL_KV_APPEND_BAD);
+    if ((f & 31u) < 10) t_fail(s, MR_FAIL_KV_MISSING);
+  }
+  t_end(s);
+}
+
+static void scn_kv_one_partition(OSim* s) { /* one_partition_3a, kvraft/tests.rs:276-342 */
+  uint32_t n = s->n, all = (1u << n) - 1;
+  t_new(s, 0);
+  s->kv_mode = 1;
+  s->th[0].live = 1;
+  main_clerk(s, 0, 0, all);
+  main_call(s, KV_PUT, 1, TOK_NUM(13));
+  uint32_t leader = kv_leader(s), a[MR_MAX_NODES], m = n; /* make_partition (tester.rs:184-192) */
+  if (leader == ~0u) leader = 0;
+  for (uint32_t i = 0; i < n; i++) a[i] = i;
+  a[leader] = a[m - 1]; m--; /* swap_remove(leader) */
+  uint32_t p1 = 0, p2 = 1u << leader;
+  for (uint32_t i = 0; i < m; i++) { if (i < n / 2 + 1) p1 |= 1u << a[i]; else p2 |= 1u << a[i]; }
+  t_partition(s, p1, p2);
+  main_clerk(s, 1, 1, p1); /* ckp1 */
+  task_clerk(s, 2, 2, p2);  /* ckp2a */
+  task_clerk(s, 3, 3, p2);  /* ckp2b */
+  main_callk(s, 1, KV_PUT, 1, TOK_NUM(14));
+  t_check(s, 1, 1, TOK_NUM(14));
+  kv_task_spawn(s, 2, 1, 3, 0, KV_PUT, 1, TOK_NUM(15), 1); /* ckp2a.put("1", "15") */
+  kv_task_spawn(s, 3, 2, 3, 0, KV_GET, 1, 0, 1);           /* ckp2b.get("1") */
+  s->main_join = JOIN_ANY; s->mwake = s->now + 1000000u; /* select! { put, get, sleep(1 s) } */
+  main_block(s);
+  s->main_join = ~0u;
+  if (!s->th[2].live || !s->th[3].live) t_fail(s, MR_FAIL_KV_MINORITY_PROGRESS);
+  t_check(s, 1, 1, TOK_NUM(14));
+  main_callk(s, 1, KV_PUT, 1, TOK_NUM(16));
+  t_check(s, 1, 1, TOK_NUM(16));
+  t_connect_all(s);
+  t_connect_client(s, 2, all);
+  t_connect_client(s, 3, all);
+  t_sleep(s, ELECTION_US);
+  if (s->th[2].live && s->th[3].live) { /* select! { sleep(3 s), put, get } */
+    s->main_join = JOIN_ANY; s->mwake = s->now + 3000000u;
+    main_block(s);
+    s->main_join = ~0u;
+    if (s->th[2].live && s->th[3].live) t_fail(s, MR_FAIL_KV_NO_COMPLETION);
+  }
+  t_check(s, 0, 1, TOK_NUM(15));
+  t_end(s);
+}
+
+static void scn_kv_snapshot_rpc(OSim* s) { /* snapshot_rpc_3b, kvraft/tests.rs:396-454 */
+  s->kv_maxraft = 1000;
+  t_new(s, 0);
+  s->kv_mode = 1;
+  s->th[0].live = 1;
+  main_clerk(s, 0, 0, 7u);
+  main_call(s, KV_PUT, KEY_LETTER('a'), TOK_LETTER('A'));
+  t_check(s, 0, KEY_LETTER('a'), TOK_LETTER('A'));
+  t_partition(s, 3u, 4u); /* [0, 1] | [2] */
+  main_clerk(s, 1, 1, 3u);
+  for (uint32_t i = 0; i < 50; i++) main_callk(s, 1, KV_PUT, i, TOK_NUM(i));
+  t_sleep(s, ELECTION_US);
+  main_callk(s, 1, KV_PUT, KEY_LETTER('b'), TOK_LETTER('B'));
+  if (t_log_size(s) > 2 * s->kv_maxraft) t_fail(s, MR_FAIL_KV_LOG_SIZE);
+  t_partition(s, 5u, 2u); /* [0, 2] | [1] */
+  main_clerk(s, 2, 2, 5u);
+  main_callk(s, 2, KV_PUT, KEY_LETTER('c'), TOK_LETTER('C'));
+  main_callk(s, 2, KV_PUT, KEY_LETTER('d'), TOK_LETTER('D'));
+  t_check(s, 2, KEY_LETTER('a'), TOK_LETTER('A'));
+  t_check(s, 2, KEY_LETTER('b'), TOK_LETTER('B'));
+  t_check(s, 2, 1, TOK_NUM(1));
+  t_check(s, 2, 49, TOK_NUM(49));
+  t_partition(s, 7u, 0u);
+  main_call(s, KV_PUT, KEY_LETTER('e'), TOK_LETTER('E'));
+  t_check(s, 0, KEY_LETTER('c'), TOK_LETTER('C'));
+  t_check(s, 0, KEY_LETTER('e'), TOK_LETTER('E'));
+  t_check(s, 0, 1, TOK_NUM(1));
+  t_end(s);
+}
+
+static void scn_kv_snapshot_size(OSim* s) { /* snapshot_size_3b, kvraft/tests.rs:456-492 */
+  s->kv_maxraft = 1000;
+  t_new(s, 0);
+  s->kv_mode = 1;
+  s->th[0].live = 1;
+  main_clerk(s, 0, 0, 7u);
+  const uint32_t X = KEY_LETTER('x');
+  for (int i = 0; i < 200; i++) {
+    main_call(s, KV_PUT, X, TOK_NUM(0));
+    t_check(s, 0, X, TOK_NUM(0));
+    main_call(s, KV_PUT, X, TOK_NUM(1));
+    t_check(s, 0, X, TOK_NUM(1));
+  }
+  if (t_log_size(s) > 2 * s->kv_maxraft) t_fail(s, MR_FAIL_KV_LOG_SIZE);
+  uint32_t mx = 0;
+  for (uint32_t i = 0; i < s->n; i++) { uint32_t z = kv_snap_size(&s->kvs[i]); if (z > mx) mx = z; }
+  if (mx > 500) t_fail(s, MR_FAIL_KV_SNAPSHOT_SIZE);
+  t_end(s);
 }
 
 /* kvraft/tester.rs:153-169: the KV server's state machine is volatile (rebuilt by
@@ -1905,6 +2089,7 @@ static void ct_spawn(OSim* s, uint32_t slot, uint32_t tid, uint32_t gid) {
   s->th[slot].cli = gid;
   memset(&s->ck[slot], 0, sizeof s->ck[slot]);
   s->ck[slot].id = tid; /* cka = t.make_client() */
+  s->ck[slot].owner = slot;
 }
 
 static void scn_ctrl_basic(OSim* s) { /* basic_4a, shard_ctrler/tests.rs:24-166 */
@@ -2065,6 +2250,10 @@ static int run_scenario(OSim* s) {
     case MR_SCN_KV_PERSIST_CONCURRENT_UNRELIABLE_3A: scn_kv_generic(s, 5, 1, 1, 0, 0); break;
     case MR_SCN_KV_PERSIST_PARTITION_3A: scn_kv_generic(s, 5, 0, 1, 1, 0); break;
     case MR_SCN_KV_PERSIST_PARTITION_UNRELIABLE_3A: scn_kv_generic(s, 5, 1, 1, 1, 0); break;
+    case MR_SCN_KV_UNRELIABLE_ONE_KEY_3A: scn_kv_one_key(s); break;
+    case MR_SCN_KV_ONE_PARTITION_3A: scn_kv_one_partition(s); break;
+    case MR_SCN_KV_SNAPSHOT_RPC_3B: scn_kv_snapshot_rpc(s); break;
+    case MR_SCN_KV_SNAPSHOT_SIZE_3B: scn_kv_snapshot_size(s); break;
     case MR_SCN_KV_SNAPSHOT_RECOVER_3B: scn_kv_generic(s, 1, 0, 1, 0, 1000); break;
     case MR_SCN_KV_SNAPSHOT_RECOVER_MANY_CLIENTS_3B: scn_kv_generic(s, 20, 0, 1, 0, 1000); break;
     case MR_SCN_KV_SNAPSHOT_UNRELIABLE_3B: scn_kv_generic(s, 5, 1, 0, 0, 1000); break;
@@ -2137,6 +2326,7 @@ static void sim_reset(OSim* s, uint64_t cluster) {
   memset(s->kvs, 0, MR_MAX_NODES * sizeof(OKvState));
   memset(s->kring_idx, 0, KV_RING * sizeof(uint32_t));
   memset(s->link, 0xFF, sizeof s->link);
+  memset(s->ccut, 0, sizeof s->ccut);
   for (uint32_t i = 0; i < MR_MAX_NODES; i++) { /* the initial config, num 0 */
     s->ncfg[i] = 1;
     memset(&s->cfgs[i * CFG_CAP], 0, sizeof(OCfg));
