@@ -33,23 +33,27 @@ N_GROUPS = 8
 DEFAULT_N = [0, 3, 3, 7, 5, 3, 5, 3, 3, 5, 3, 3, 5, 3, 5, 5, 5, 5, 5, 3, 3, 3, 3, 3, 5, 5, 5, 5, 3, 3, 5, 5, 5, 5, 5, 5, 5, 3, 5, 3, 3, 5, 5, 5, 5, 5]
 
 
-def _units(csrc):
+def _units(csrc, scns=None):
     kern = os.path.join(csrc, "mr_kernel.hip")
     units = [(kern, "common", ["-DMR_COMMON=1", "-DMR_SCN_LIST=", "-DMR_NB=8"])]
     for nb in (3, 5, 8):
-        ids = [i for i in SCN_IDS if nb == 8 or DEFAULT_N[i] == nb]
+        ids = [i for i in (scns or SCN_IDS) if nb == 8 or DEFAULT_N[i] == nb]
+        if not ids:
+            continue
         ng = max(1, min(N_GROUPS, (len(ids) + 2) // 3))
         for g in range(ng):
             lst = " ".join(f"MR_INST({i})" for i in ids[g::ng])
             units.append((kern, f"nb{nb}_{g}", ["-DMR_COMMON=0", f"-DMR_SCN_LIST={lst}",
                                                 f"-DMR_NB={nb}"]))
+    host = ["-DMR_DEV_SCNS=" + " ".join(f"MR_INST({i})" for i in scns)] if scns else []
     for src in sorted(glob.glob(os.path.join(csrc, "*.cpp"))):
-        units.append((src, os.path.splitext(os.path.basename(src))[0], []))
+        units.append((src, os.path.splitext(os.path.basename(src))[0], host))
     return units
 
 
-def build_hip(force=False, verbose=False, extra=(), out=None):
-    """Compile the product library; `extra` flags / `out` path for dev variants."""
+def build_hip(force=False, verbose=False, extra=(), out=None, scns=None):
+    """Compile the product library; `extra` flags / `out` path / only scenario ids `scns`
+    for dev variants."""
     out = out or LIB
     csrc = os.path.join(HERE, "csrc")
     srcs = sorted(glob.glob(os.path.join(csrc, "*.hip")) + glob.glob(os.path.join(csrc, "*.cpp")))
@@ -63,7 +67,7 @@ def build_hip(force=False, verbose=False, extra=(), out=None):
             "-Wno-unused-function", *extra]
     jobs, objs, running = [], [], []
     njobs = max(1, min(16, os.cpu_count() or 1))
-    for src, name, flags in _units(csrc):
+    for src, name, flags in _units(csrc, scns):
         obj = os.path.join(objdir, name + ".o")
         objs.append(obj)
         cmd = base + flags + ["-c", src, "-o", obj]

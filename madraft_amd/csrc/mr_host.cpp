@@ -22,7 +22,11 @@ hipError_t launch_step(const Dev& D, uint32_t scn, uint32_t budget, hipStream_t 
   case S:                                                                           \
     return D.n <= nb_of(S) ? launch_step_t<S, nb_of(S)>(D, budget, s)              \
                            : launch_step_t<S, MR_MAX_NODES>(D, budget, s);
+#ifdef MR_DEV_SCNS  // dev variants built for a few scenarios (build.py scns=)
+    MR_DEV_SCNS
+#else
     MR_ALL_SCNS
+#endif
 #undef MR_INST
     default: return hipErrorInvalidValue;
   }

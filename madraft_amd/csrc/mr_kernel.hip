@@ -192,6 +192,34 @@ DI void store_node(const Dev& D, const X& x, uint32_t d, const NC& n) {
   p[1] = make_uint4(n.last, n.snap, n.snapt, n.ectr);
   p[2] = make_uint4(n.nctr, n.pexp, n.slen, n.lastt);
 }
+// next[] / match[] of a node (words 16..31), loaded with its scalars at the start of
+// every node event: a leader's sends and acknowledgements then wait on no further load
+struct PV {
+  uint32_t nx[NB], mt[NB];
+};
+DI void load_peers(const Dev& D, const X& x, uint32_t d, PV& pv) {
+  const uint4* p = reinterpret_cast<const uint4*>(NDP(d) + NR_PEER);
+#pragma unroll
+  for (uint32_t q = 0; q < (NB + 3) / 4; q++) {
+    const uint4 a = p[q], b = p[MR_MAX_NODES / 4 + q];
+    const uint32_t an[4] = {a.x, a.y, a.z, a.w}, bm[4] = {b.x, b.y, b.z, b.w};
+#pragma unroll
+    for (uint32_t r = 0; r < 4; r++)
+      if (4 * q + r < NB) { pv.nx[4 * q + r] = an[r]; pv.mt[4 * q + r] = bm[r]; }
+  }
+}
+// v[i] for a per-lane index, as a select chain over constant indices (no scratch)
+DI uint32_t sel_nb(const uint32_t (&v)[NB], uint32_t i) {
+  uint32_t r = 0;
+#pragma unroll
+  for (uint32_t q = 0; q < NB; q++) r = q == i ? v[q] : r;
+  return r;
+}
+DI void put_nb(uint32_t (&v)[NB], uint32_t i, uint32_t val) {
+#pragma unroll
+  for (uint32_t q = 0; q < NB; q++) v[q] = q == i ? val : v[q];
+}
+
 DI uint32_t term_at(const Dev& D, const X& x, uint32_t d, const NC& n, uint32_t i) {
   if (i == 0) return 0;
   if (i == n.snap) return n.snapt;
@@ -359,7 +387,10 @@ DI void guard_log_write(const Dev& D, X& x, uint32_t L, uint32_t& pexp, uint32_t
 }
 
 // ---------------------------------------------------------------- tester storage
-constexpr uint32_t AC = 4;  // entries per batch of independent loads in log walks
+#ifndef MR_AC
+#define MR_AC 8
+#endif
+constexpr uint32_t AC = MR_AC;  // entries per batch of independent loads in log walks
 #ifndef MR_AC_APPLY
 #define MR_AC_APPLY 8
 #endif
@@ -491,20 +522,20 @@ DI void safety_on_leader(const Dev& D, X& x, uint32_t me, const NC& d) {
 // AppendEntries / InstallSnapshot acknowledgement up to xv; returns the peer
 // mask to send a follow-up append to. The match indices of every peer and
 // next[p] are loaded as one batch of independent loads.
-DI uint32_t on_ack(const Dev& D, X& x, uint32_t me, NC& d, uint32_t p, uint32_t xv) {
+DI uint32_t on_ack(const Dev& D, X& x, uint32_t me, NC& d, uint32_t p, uint32_t xv, PV& pv) {
   // constant indices only: a select chain over a per-lane index is turned
   // back into a dynamically indexed scratch array by the compiler
-  uint32_t mv[NB], mp = 0, lbase = 0;
+  uint32_t mv[NB], mp = 0, lbase = 0, nx = 0;
 #pragma unroll
   for (uint32_t q = 0; q < NB; q++) {
-    const uint32_t v = q < D.n ? PR(PF_MATCH, me, q) : 0u;  // match[me] = the leader base
+    const uint32_t v = q < D.n ? pv.mt[q] : 0u;  // match[me] = the leader base
     mp = (q == p) ? v : mp;
+    nx = (q == p) ? pv.nx[q] : nx;
     lbase = (q == me) ? v : lbase;
     mv[q] = (q == me) ? d.last : ((q == p && xv > v) ? xv : v);
   }
-  uint32_t nx = PR(PF_NEXT, me, p);
-  if (xv > mp) PR(PF_MATCH, me, p) = xv;
-  if (xv + 1 > nx) { nx = xv + 1; PR(PF_NEXT, me, p) = nx; }
+  if (xv > mp) { PR(PF_MATCH, me, p) = xv; put_nb(pv.mt, p, xv); }
+  if (xv + 1 > nx) { nx = xv + 1; PR(PF_NEXT, me, p) = nx; put_nb(pv.nx, p, nx); }
   advance_commit(D, x, me, d, mv, lbase);
   return nx <= d.last ? (1u << p) : 0u;  // still behind: pipeline the next batch
 }
@@ -550,6 +581,8 @@ DI void node_event(const Dev& D, X& x, bool is_msg, uint32_t tnode, uint32_t slo
     }
   }
   NC d = load_node(D, x, me);
+  PV pv;
+  load_peers(D, x, me, pv);
   PROF(P_LOAD);
   uint32_t mode = SEND_NONE, peers = 0, rtype = 0, ra = 0, rb = 0, kind;
   const uint32_t others = ((1u << D.n) - 1u) & ~(1u << me);
@@ -611,9 +644,13 @@ DI void node_event(const Dev& D, X& x, bool is_msg, uint32_t tnode, uint32_t slo
             }
             d.f = f_set(d.f, 0, 2, R_L);
             CADD(CNT_LEADERS, 1u);
-            for (uint32_t p = 0; p < D.n; p++) {
-              PR(PF_NEXT, me, p) = d.last + 1;
-              PR(PF_MATCH, me, p) = (p == me) ? d.last : 0u;
+#pragma unroll
+            for (uint32_t p = 0; p < NB; p++) {
+              if (p >= D.n) break;
+              pv.nx[p] = d.last + 1;
+              pv.mt[p] = (p == me) ? d.last : 0u;
+              PR(PF_NEXT, me, p) = pv.nx[p];
+              PR(PF_MATCH, me, p) = pv.mt[p];
             }
             set_timer(x, me, x.now + D.hb);
             mode = SEND_APPEND; peers = others;
@@ -673,12 +710,13 @@ DI void node_event(const Dev& D, X& x, bool is_msg, uint32_t tnode, uint32_t slo
         if (role != R_L || mterm != term) break;
         mode = SEND_APPEND;
         if (ma) {
-          peers = on_ack(D, x, me, d, src, mb);
+          peers = on_ack(D, x, me, d, src, mb, pv);
         } else {
-          uint32_t xx = mb, lo = PR(PF_MATCH, me, src) + 1, hi = d.last + 1;
+          uint32_t xx = mb, lo = sel_nb(pv.mt, src) + 1, hi = d.last + 1;
           if (xx < lo) xx = lo;
           if (xx > hi) xx = hi;
           PR(PF_NEXT, me, src) = xx;
+          put_nb(pv.nx, src, xx);
           peers = 1u << src;
         }
         PROF(P_AEREP);
@@ -707,7 +745,7 @@ DI void node_event(const Dev& D, X& x, bool is_msg, uint32_t tnode, uint32_t slo
       case M_IS_REP:
         if (role == R_L && mterm == term && mb > 0) {
           mode = SEND_APPEND;
-          peers = on_ack(D, x, me, d, src, mb);
+          peers = on_ack(D, x, me, d, src, mb, pv);
         }
         PROF(P_ISREP);
         break;
@@ -739,10 +777,10 @@ DI void node_event(const Dev& D, X& x, bool is_msg, uint32_t tnode, uint32_t slo
   if (mode == SEND_APPEND) {  // only a leader appends
     uint32_t nxa[NB];
     bool any_is = false;
-    const uint32_t lbase = PR(PF_MATCH, me, me);
+    const uint32_t lbase = sel_nb(pv.mt, me);
 #pragma unroll
     for (uint32_t p = 0; p < NB; p++) {
-      nxa[p] = bit(peers, p) ? PR(PF_NEXT, me, p) : 0u;
+      nxa[p] = bit(peers, p) ? pv.nx[p] : 0u;
       any_is |= bit(peers, p) && nxa[p] <= d.snap;
     }
 #pragma unroll
