@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define MR_ABI_VERSION 1u
+#define MR_ABI_VERSION 2u
 #define MR_MAX_NODES 8u
 #define MR_MAX_MSG_SLOTS 64u
 #define MR_MAX_AE 32u
@@ -119,6 +119,7 @@ static inline uint32_t mr_kv_log_cap(uint32_t s) {
  * way the reference tester grades a student's raft.rs */
 #define MR_F_BUG_VOTE_TWICE 0x10u /* voters ignore votedFor: two leaders per term possible */
 #define MR_F_BUG_VOTE_STALE 0x20u /* voters skip the up-to-date check (Raft §5.4.1) */
+#define MR_F_BUG_NO_PREV_CHECK 0x40u /* followers skip AppendEntries' prevLogTerm check (§5.3) */
 
 /* ---- verdicts: one code per tester panic site ---- */
 enum mr_fail {
@@ -172,6 +173,7 @@ enum mr_fail {
   MR_FAIL_KV_MINORITY_PROGRESS = 46, /* kvraft/tests.rs:315-319 */
   MR_FAIL_KV_NO_COMPLETION = 47,     /* kvraft/tests.rs:333-337 */
   MR_FAIL_KV_CHECK = 48,             /* kvraft/tester.rs:266-271 Clerk::check */
+  MR_FAIL_SAFETY_LOG_MATCHING = 49,  /* MR_F_SAFETY: same index and term, different command */
   /* simulator limits (not reference panics): a cluster that hits one is reported, never passed */
   MR_FAIL_SIM_CAPACITY = 60,      /* a log / apply / sequence capacity of the config was exceeded */
   MR_FAIL_SIM_EVENT_LIMIT = 61,   /* cfg.max_events processed without a verdict */
@@ -219,6 +221,9 @@ typedef struct mr_counters {
   uint64_t first_fail_cluster; /* global cluster id (UINT64_MAX if none) */
   uint64_t first_fail_code;
   uint64_t fail_hist[64];  /* verdict histogram by code (index 63 = >= 63) */
+  /* coverage histograms over clusters, bucket b = 0 for 0, else min(15, 1 + floor(log2 v)) */
+  uint64_t cov_leaders[16]; /* leaders elected per cluster */
+  uint64_t cov_events[16];  /* events per cluster */
 } mr_counters;
 
 typedef struct mr_run_stats {

@@ -7,7 +7,7 @@ import ctypes as C
 
 import numpy as np
 
-MR_ABI_VERSION = 1
+MR_ABI_VERSION = 2
 MR_MAX_NODES = 8
 MR_RUNNING = 0xFFFF
 MR_PASS = 0
@@ -18,6 +18,7 @@ MR_F_TRACE = 0x4
 MR_F_SAFETY = 0x8
 MR_F_BUG_VOTE_TWICE = 0x10
 MR_F_BUG_VOTE_STALE = 0x20
+MR_F_BUG_NO_PREV_CHECK = 0x40
 
 README_SEED = 1629626496  # /root/reference/README.md:48
 
@@ -64,7 +65,7 @@ FAIL_NAMES = {
     37: "CTRL_MOVE_WRONG", 38: "CTRL_MINIMAL_JOIN", 39: "CTRL_MINIMAL_LEAVE", 40: "CTRL_NO_LEADER",
     41: "CTRL_SAME_CONFIG", 42: "SAFETY_ELECTION", 43: "SAFETY_COMPLETENESS",
     44: "KV_LOG_SIZE", 45: "KV_SNAPSHOT_SIZE", 46: "KV_MINORITY_PROGRESS", 47: "KV_NO_COMPLETION",
-    48: "KV_CHECK", 60: "SIM_CAPACITY",
+    48: "KV_CHECK", 49: "SAFETY_LOG_MATCHING", 60: "SIM_CAPACITY",
     61: "SIM_EVENT_LIMIT", 62: "SIM_BAD_PROGRAM", 0xFFFF: "RUNNING",
 }
 
@@ -87,13 +88,22 @@ class MrCounters(C.Structure):
         "msgs_sent", "drop_clog", "drop_loss", "drop_overflow", "drop_deliver", "drop_stale",
         "elections", "leaders_elected", "applies", "snapshots", "installs", "entries_shipped",
         "virt_time_us", "max_inflight", "max_log", "max_index", "first_fail_cluster",
-        "first_fail_code")] + [("fail_hist", C.c_uint64 * 64)]
+        "first_fail_code")] + [("fail_hist", C.c_uint64 * 64), ("cov_leaders", C.c_uint64 * 16),
+                               ("cov_events", C.c_uint64 * 16)]
 
     def to_dict(self):
-        d = {n: getattr(self, n) for n, _ in self._fields_ if n != "fail_hist"}
+        d = {n: getattr(self, n) for n, _ in self._fields_
+             if n not in ("fail_hist", "cov_leaders", "cov_events")}
         d["fail_hist"] = {FAIL_NAMES.get(i, str(i)): int(v)
                           for i, v in enumerate(self.fail_hist) if v}
+        d["cov_leaders"] = [int(v) for v in self.cov_leaders]
+        d["cov_events"] = [int(v) for v in self.cov_events]
         return d
+
+
+def cov_bucket(v):
+    """Coverage-histogram bucket of a per-cluster count (mr_counters.cov_*)."""
+    return 0 if v == 0 else min(15, int(v).bit_length())
 
 
 class MrRunStats(C.Structure):

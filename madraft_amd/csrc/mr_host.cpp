@@ -72,7 +72,7 @@ const uint8_t k_nodes[MR_SCN_COUNT_] = {0, 3, 3, 7, 5, 3, 5, 3, 3, 5, 3, 3, 5, 3
                                         5, 5, 5, 5, 5, 3, 3, 3, 3, 3, 5, 5, 5, 5, 3, 3,
                                         5, 5, 5, 5, 5, 5, 5, 3, 5, 3, 3, 5, 5, 5, 5, 5};
 
-constexpr size_t RED_N = CNT__N + 8 + 64;  // reduce_kernel output slots
+constexpr size_t RED_N = CNT__N + 8 + 64 + 32;  // reduce_kernel output slots
 }  // namespace
 
 struct mr_batch {
@@ -151,6 +151,7 @@ const char* mr_fail_message(uint32_t code) {
     case MR_FAIL_KV_MINORITY_PROGRESS: return "put/get in minority completed";
     case MR_FAIL_KV_NO_COMPLETION: return "put/get did not complete";
     case MR_FAIL_KV_CHECK: return "get(key) check failed";
+    case MR_FAIL_SAFETY_LOG_MATCHING: return "log matching: same index and term, different entries";
     case MR_FAIL_SIM_CAPACITY: return "simulator capacity exceeded";
     case MR_FAIL_SIM_EVENT_LIMIT: return "simulator event limit exceeded";
     case MR_FAIL_SIM_BAD_PROGRAM: return "scenario program error";
@@ -222,7 +223,7 @@ int mr_batch_create(const mr_cfg* cfg, mr_batch** out) {
   D.null_raft = (cfg->flags & MR_F_NULL_RAFT) ? 1u : 0u;
   D.unrel_flag = (cfg->flags & MR_F_UNRELIABLE) ? 1u : 0u;
   D.safety = (cfg->flags & MR_F_SAFETY) ? 1u : 0u;
-  D.bugs = cfg->flags & (MR_F_BUG_VOTE_TWICE | MR_F_BUG_VOTE_STALE);
+  D.bugs = cfg->flags & (MR_F_BUG_VOTE_TWICE | MR_F_BUG_VOTE_STALE | MR_F_BUG_NO_PREV_CHECK);
   D.links = kv_gen(cfg->scenario).part ? 1u : 0u;  // server-link cuts (CS_CUT) can exist
   D.trace_clusters = (cfg->flags & MR_F_TRACE) ? cfg->trace_clusters : 0u;
   D.trace_cap = cfg->trace_cap;
@@ -409,6 +410,10 @@ int mr_batch_counters(mr_batch* b, mr_counters* out) {
   out->done = h[CNT__N + 3]; out->passed = h[CNT__N + 4]; out->failed = out->done - out->passed;
   out->first_fail_cluster = h[CNT__N + 5];
   for (int i = 0; i < 64; i++) out->fail_hist[i] = h[CNT__N + 8 + i];
+  for (int i = 0; i < 16; i++) {
+    out->cov_leaders[i] = h[CNT__N + 72 + i];
+    out->cov_events[i] = h[CNT__N + 88 + i];
+  }
   out->first_fail_code = 0;
   if (out->first_fail_cluster != ~0ull) {
     uint32_t code = 0;

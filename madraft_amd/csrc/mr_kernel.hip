@@ -679,7 +679,7 @@ DI void node_event(const Dev& D, X& x, bool is_msg, uint32_t tnode, uint32_t slo
         const uint32_t tp = term_at(D, x, me, d, prev);
         ae_load_batch(D, x, me, d, src, mat, pp, ma, k, j0, pe, lt);
         PROF(P_AE_PROBE);
-        if (tp != pterm) {
+        if (!(D.bugs & MR_F_BUG_NO_PREV_CHECK) && tp != pterm) {
           uint32_t xx = prev;
           while (xx - 1 > d.snap && term_at(D, x, me, d, xx - 1) == tp) xx--;
           rb = xx;
@@ -691,7 +691,14 @@ DI void node_event(const Dev& D, X& x, bool is_msg, uint32_t tnode, uint32_t slo
           for (uint32_t q = 0; q < AC; q++) {
             const uint32_t jx = j + q, i = ma + 1 + jx;
             if (jx >= k) break;
-            if (i <= d.last && lt[q] == pe[q].term) continue;  // d.last only drops below i here
+            if (i <= d.last && lt[q] == pe[q].term) {  // d.last only drops below i here
+              // MR_F_SAFETY log matching: an entry with the same index and term is the same entry
+              if (D.safety && D.log[logi(D, x, me, i)].val != pe[q].val) {
+                fail(D, x, MR_FAIL_SAFETY_LOG_MATCHING);
+                return;
+              }
+              continue;
+            }
             if (i - d.snap > D.log_cap) { fail(D, x, MR_FAIL_SIM_CAPACITY); return; }
             guard_log_write(D, x, me, d.pexp, i);
             D.log[logi(D, x, me, i)] = pe[q];
@@ -1179,8 +1186,9 @@ __global__ void __launch_bounds__(256) reset_kernel(Dev D) {
 // cluster; out[] layout documented in mr_host.cpp (RED_*)
 __global__ void __launch_bounds__(256) reduce_kernel(Dev D, unsigned long long* out,
                                                     uint64_t cluster_base) {
-  __shared__ unsigned long long acc[CNT__N + 8 + 64];
-  for (uint32_t i = threadIdx.x; i < CNT__N + 8 + 64; i += blockDim.x) acc[i] = 0;
+  constexpr uint32_t RN = CNT__N + 8 + 64 + 32;  // counters, scalars, verdicts, coverage
+  __shared__ unsigned long long acc[RN];
+  for (uint32_t i = threadIdx.x; i < RN; i += blockDim.x) acc[i] = 0;
   __syncthreads();
   X x;
   x.c = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1197,11 +1205,14 @@ __global__ void __launch_bounds__(256) reduce_kernel(Dev D, unsigned long long* 
     atomicAdd(&acc[CNT__N + 3], code != RUN ? 1ull : 0ull);
     atomicAdd(&acc[CNT__N + 4], code == MR_PASS ? 1ull : 0ull);
     if (code != RUN) atomicAdd(&acc[CNT__N + 8 + (code < 63 ? code : 63)], 1ull);
+    auto bucket = [](uint32_t v) { return v == 0 ? 0u : min(15u, 32u - (uint32_t)__builtin_clz(v)); };
+    atomicAdd(&acc[CNT__N + 72 + bucket(CS(CS_CNT + CNT_LEADERS))], 1ull);
+    atomicAdd(&acc[CNT__N + 88 + bucket(CS(CS_EVENTS))], 1ull);
     if (code != RUN && code != MR_PASS)
       atomicMin(&out[CNT__N + 5], (unsigned long long)(cluster_base + x.c));
   }
   __syncthreads();
-  for (uint32_t i = threadIdx.x; i < CNT__N + 8 + 64; i += blockDim.x) {
+  for (uint32_t i = threadIdx.x; i < RN; i += blockDim.x) {
     if (i == CNT__N + 5 || i == CNT__N + 6 || i == CNT__N + 7) continue;
     if (acc[i] == 0) continue;
     if (i >= CNT_MAX_INFLIGHT && i < CNT__N) atomicMax(&out[i], acc[i]);

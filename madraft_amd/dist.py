@@ -5,7 +5,7 @@ in-scope test — so rank r of W owns the contiguous global
 cluster range shard(total, W, r) and runs the identical kernel on it. Seeds
 derive from global cluster ids, so results do not depend on W. The only
 collective is one all-reduce of the batch counters at the end: sum for
-counts, max for maxima, min for the first failing global cluster id. With
+counts, verdict and coverage histograms, max for maxima, min for the first failing global cluster id. With
 backend "nccl" that all-reduce is RCCL over xGMI; a few hundred bytes,
 latency-bound. Tests run the same code with gloo on CPU.
 """
@@ -19,6 +19,7 @@ SUM_KEYS = ["clusters", "done", "passed", "failed", "events", "ev_msg", "ev_time
             "elections", "leaders_elected", "applies", "snapshots", "installs",
             "entries_shipped", "virt_time_us"]
 MAX_KEYS = ["max_inflight", "max_log", "max_index"]
+COV_KEYS = ["cov_leaders", "cov_events"]
 NO_FAIL = (1 << 63) - 1
 
 
@@ -42,13 +43,18 @@ def allreduce_counters(c, device=None, group=None):
     h = torch.zeros(len(names), dtype=torch.int64, device=dev)
     for name, v in c.get("fail_hist", {}).items():
         h[[k for k, _ in names].index(code_of[name])] = int(v)
-    s = torch.cat([s, h])
+    cov = torch.tensor([int(v) for k in COV_KEYS for v in c.get(k, [0] * 16)], dtype=torch.int64,
+                       device=dev)
+    s = torch.cat([s, h, cov])
     dist.all_reduce(s, op=dist.ReduceOp.SUM, group=group)
     dist.all_reduce(m, op=dist.ReduceOp.MAX, group=group)
     dist.all_reduce(f, op=dist.ReduceOp.MIN, group=group)
     out = dict(c)
     sl = s.tolist()
     out["fail_hist"] = {name: int(v) for (_, name), v in zip(names, sl[len(SUM_KEYS):]) if v}
+    base = len(SUM_KEYS) + len(names)
+    for j, k in enumerate(COV_KEYS):  # coverage histograms
+        out[k] = [int(v) for v in sl[base + 16 * j: base + 16 * (j + 1)]]
     out.update({k: int(v) for k, v in zip(SUM_KEYS, sl)})
     out.update({k: int(v) for k, v in zip(MAX_KEYS, m.tolist())})
     out["first_fail_cluster"] = None if int(f.item()) == NO_FAIL else int(f.item())

@@ -731,7 +731,7 @@ static void deliver(OSim* s, OMsg* m) {
         prev = d->snap_idx; pterm = d->snap_term;
       }
       if (prev > d->last) { reply(s, me, m, M_AE_REP, 0, d->last + 1); break; }
-      if (term_at(s, d, prev) != pterm) {
+      if (!(s->cfg.flags & MR_F_BUG_NO_PREV_CHECK) && term_at(s, d, prev) != pterm) {
         uint32_t ct = term_at(s, d, prev), x = prev;
         while (x - 1 > d->snap_idx && term_at(s, d, x - 1) == ct) x--;
         reply(s, me, m, M_AE_REP, 0, x);
@@ -739,7 +739,12 @@ static void deliver(OSim* s, OMsg* m) {
       }
       for (uint32_t j = j0; j < m->k; j++) {
         uint32_t i = m->a + 1 + j;
-        if (i <= d->last && term_at(s, d, i) == m->et[j]) continue;
+        if (i <= d->last && term_at(s, d, i) == m->et[j]) {
+          /* MR_F_SAFETY log matching: an entry with the same index and term is the same entry */
+          if ((s->cfg.flags & MR_F_SAFETY) && d->lval[lpos(s, i)] != m->ev[j])
+            t_fail(s, MR_FAIL_SAFETY_LOG_MATCHING);
+          continue;
+        }
         log_put(s, d, i, m->et[j], m->ev[j]); /* truncates to i-1, appends */
       }
       uint32_t lc = m->a + m->k;
@@ -2470,6 +2475,7 @@ const char* mro_fail_message(uint32_t code) {
     case MR_FAIL_KV_MINORITY_PROGRESS: return "put/get in minority completed";
     case MR_FAIL_KV_NO_COMPLETION: return "put/get did not complete";
     case MR_FAIL_KV_CHECK: return "get(key) check failed";
+    case MR_FAIL_SAFETY_LOG_MATCHING: return "log matching: same index and term, different entries";
     case MR_FAIL_SIM_CAPACITY: return "simulator capacity exceeded";
     case MR_FAIL_SIM_EVENT_LIMIT: return "simulator event limit exceeded";
     default: return "scenario assertion failed";

@@ -139,12 +139,31 @@ def test_baseline_sizes(hip, oracle, test, clusters, kw):
     ("unreliable_3a", _abi.MR_F_SAFETY),
     ("many_election_2a", _abi.MR_F_SAFETY | _abi.MR_F_BUG_VOTE_TWICE),
     ("figure_8_2c", _abi.MR_F_SAFETY | _abi.MR_F_BUG_VOTE_STALE),
+    ("rejoin_2b", _abi.MR_F_SAFETY | _abi.MR_F_BUG_NO_PREV_CHECK),
 ])
 def test_safety_checks_bit_exact(hip, oracle, test, flags):
     """MR_F_SAFETY checks (and the buggy-Raft variants they catch) on the GPU:
     same verdicts, times and traces as the oracle."""
     code, _ = compare(hip, oracle, test, 512, flags=flags)
-    if flags & (_abi.MR_F_BUG_VOTE_TWICE | _abi.MR_F_BUG_VOTE_STALE):
-        assert np.isin(code, [42, 43]).sum() >= 10
+    if flags & (_abi.MR_F_BUG_VOTE_TWICE | _abi.MR_F_BUG_VOTE_STALE | _abi.MR_F_BUG_NO_PREV_CHECK):
+        assert (code != 0).sum() >= 10
     else:
-        assert not np.isin(code, [42, 43]).any()
+        assert not np.isin(code, [42, 43, 49]).any()
+
+
+@pytest.mark.parametrize("test", ["figure_8_unreliable_2c", "unreliable_3a"])
+def test_coverage_histograms(hip, oracle, test):
+    """mr_counters.cov_*: per-cluster leaders elected / events in log2 buckets, equal to the
+    histograms of the oracle's per-cluster results."""
+    n = 128
+    with hip.Batch(test, n) as b:
+        b.run()
+        cnt = b.counters()
+        cfg = b.cfg
+    lead, ev = [0] * 16, [0] * 16
+    for c in range(n):
+        r, _ = oracle.run_cluster(cfg, c)
+        lead[_abi.cov_bucket(r["leaders_elected"])] += 1
+        ev[_abi.cov_bucket(r["events"])] += 1
+    assert cnt["cov_leaders"] == lead and cnt["cov_events"] == ev
+    assert sum(lead) == n

@@ -135,7 +135,7 @@ def test_safety_invariants_hold(oracle, test):
     cfg = oracle.cfg(test, flags=_abi.MR_F_SAFETY)
     code, t, dig, s = oracle.run_batch(cfg, 0, 48)
     assert (code == code0).all() and (t == t0).all() and (dig == dig0).all()
-    assert not np.isin(code, [42, 43]).any()
+    assert not np.isin(code, [42, 43, 49]).any()
     assert s["events"] == s0["events"] and s["leaders_elected"] > 0
 
 
@@ -144,6 +144,10 @@ def test_safety_invariants_hold(oracle, test):
     (_abi.MR_F_BUG_VOTE_TWICE, "figure_8_unreliable_2c", 42),
     (_abi.MR_F_BUG_VOTE_STALE, "figure_8_2c", 43),
     (_abi.MR_F_BUG_VOTE_STALE, "persist3_2c", 43),
+    # a follower that skips the prevLogTerm check breaks log matching; the apply
+    # checker (state-machine safety, tester.rs:384-388) sees it first
+    (_abi.MR_F_BUG_NO_PREV_CHECK, "figure_8_2c", 8),
+    (_abi.MR_F_BUG_NO_PREV_CHECK, "rejoin_2b", 8),
 ])
 def test_safety_catches_buggy_raft(oracle, bug, test, code_):
     """A Raft with a known voting bug is caught: with MR_F_SAFETY by the invariant
