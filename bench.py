@@ -39,7 +39,7 @@ def bytes_per_event(n):
     return 2 * (32 + 8 * n) + 64
 
 
-def cpu_baseline(test, seeds_per_proc, procs):
+def cpu_baseline(test, seeds_per_proc, procs, safety=False):
     """The oracle CLI (madsim-like scalar DES) — MADSIM_TEST_NUM seeds per
     process, one process per host core, like `MADSIM_TEST_NUM=N cargo test`."""
     exe = os.path.join(ROOT, "oracle", "_build", "mr_oracle")
@@ -50,7 +50,8 @@ def cpu_baseline(test, seeds_per_proc, procs):
     for k in range(procs):
         env = dict(os.environ, MADSIM_TEST_SEED=str(_abi.README_SEED + 10_000_000 + k * seeds_per_proc),
                    MADSIM_TEST_NUM=str(seeds_per_proc))
-        ps.append(subprocess.Popen([exe, test], env=env, stdout=subprocess.PIPE,
+        ps.append(subprocess.Popen([exe, test] + (["--safety"] if safety else []), env=env,
+                                   stdout=subprocess.PIPE,
                                    stderr=subprocess.DEVNULL, text=True))
     outs = [json.loads(p.communicate()[0].strip().splitlines()[-1]) for p in ps]
     wall = time.perf_counter() - t0
@@ -59,7 +60,8 @@ def cpu_baseline(test, seeds_per_proc, procs):
     return {"value": round(seeds / wall, 1), "unit": "seeds/s", "cores": procs, "kind": "port",
             "events_per_sec": round(events / wall, 1), "wall_s": round(wall, 3),
             "sample": f"{procs} processes x {seeds_per_proc} seeds of {test} "
-                      f"(oracle/mr_oracle, MADSIM_TEST_NUM={seeds_per_proc} each)"}
+                      f"(oracle/mr_oracle{' --safety' if safety else ''}, "
+                      f"MADSIM_TEST_NUM={seeds_per_proc} each)"}
 
 
 def load_pmc(test, clusters):
@@ -85,6 +87,8 @@ def main():
     ap.add_argument("--test", default="figure_8_unreliable_2c")
     ap.add_argument("--cpu-seeds", type=int, default=20000, help="cpu_baseline seeds per process")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-safety", action="store_true",
+                    help="without the per-event Raft invariant checks (MR_F_SAFETY)")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (RCCL) or gloo (one-GPU rehearsal)")
     a = ap.parse_args()
 
@@ -106,7 +110,8 @@ def main():
 
     total = a.clusters * world
     base, count = mdist.shard(total, world, rank)
-    b = sim.Batch(a.test, count, _abi.README_SEED, cluster_base=base, device=local)
+    b = sim.Batch(a.test, count, _abi.README_SEED, cluster_base=base, device=local,
+                  safety=not a.no_safety)
     n = int(b.cfg.n_nodes)
 
     def step(i):
@@ -167,10 +172,11 @@ def main():
         "data": "synthetic (device-generated Philox seeds; no dataset)",
         "config": {"workload": a.test, "nodes": n, "clusters_per_gpu": a.clusters,
                    "clusters_total": total, "parallelism": f"clusters sharded over {world} GPU(s)",
-                   "loss": 0.1, "latency_ms": [1, 27]},
+                   "loss": 0.1, "latency_ms": [1, 27], "safety_checks": not a.no_safety},
         "events_per_sec": round(events / elapsed, 1),
         "events_per_seed": round(events / seeds, 1),
         "pass_rate": round(passed / max(done, 1), 6),
+        "coverage": {"leaders_elected_log2": (tot if world > 1 else last)["cov_leaders"]},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
                      "traffic": traffic,
@@ -183,7 +189,7 @@ def main():
     }
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         procs = min(16, os.cpu_count() or 1)
-        out["cpu_baseline"] = cpu_baseline(a.test, a.cpu_seeds, procs)
+        out["cpu_baseline"] = cpu_baseline(a.test, a.cpu_seeds, procs, safety=not a.no_safety)
         out["gpu_over_cpu"] = round(out["value"] / out["cpu_baseline"]["value"], 2)
     if rank == 0:
         print(json.dumps(out), flush=True)

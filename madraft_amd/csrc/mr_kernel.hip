@@ -687,18 +687,25 @@ DI void node_event(const Dev& D, X& x, bool is_msg, uint32_t tnode, uint32_t slo
         }
         for (uint32_t j = j0; j < k; j += AC) {
           if (j != j0) ae_load_batch(D, x, me, d, src, mat, pp, ma, k, j, pe, lt);
+          if (D.safety) {  // MR_F_SAFETY log matching: same index and term => same entry
+            uint64_t ov[AC];  // one batch of unconditional loads (ring addresses are always valid)
+#pragma unroll
+            for (uint32_t q = 0; q < AC; q++) ov[q] = D.log[logi(D, x, me, ma + 1 + j + q)].val;
+            bool bad = false, skipping = true;  // skips form a prefix: the first write appends the rest
+#pragma unroll
+            for (uint32_t q = 0; q < AC; q++) {
+              const uint32_t i = ma + 1 + j + q;
+              const bool sk = j + q < k && i <= d.last && lt[q] == pe[q].term;
+              skipping = skipping && sk;
+              bad |= skipping && ov[q] != pe[q].val;
+            }
+            if (bad) { fail(D, x, MR_FAIL_SAFETY_LOG_MATCHING); return; }
+          }
 #pragma unroll
           for (uint32_t q = 0; q < AC; q++) {
             const uint32_t jx = j + q, i = ma + 1 + jx;
             if (jx >= k) break;
-            if (i <= d.last && lt[q] == pe[q].term) {  // d.last only drops below i here
-              // MR_F_SAFETY log matching: an entry with the same index and term is the same entry
-              if (D.safety && D.log[logi(D, x, me, i)].val != pe[q].val) {
-                fail(D, x, MR_FAIL_SAFETY_LOG_MATCHING);
-                return;
-              }
-              continue;
-            }
+            if (i <= d.last && lt[q] == pe[q].term) continue;  // d.last only drops below i here
             if (i - d.snap > D.log_cap) { fail(D, x, MR_FAIL_SIM_CAPACITY); return; }
             guard_log_write(D, x, me, d.pexp, i);
             D.log[logi(D, x, me, i)] = pe[q];

@@ -40,6 +40,7 @@ int main(int argc, char** argv) {
     else if (!strcmp(argv[i], "--iters") && i + 1 < argc) cfg.iters = (uint32_t)atoi(argv[++i]);
     else if (!strcmp(argv[i], "--unreliable")) cfg.flags |= MR_F_UNRELIABLE;
     else if (!strcmp(argv[i], "--null")) cfg.flags |= MR_F_NULL_RAFT;
+    else if (!strcmp(argv[i], "--safety")) cfg.flags |= MR_F_SAFETY;
   }
   const char* es = getenv("MADSIM_TEST_SEED");
   const char* en = getenv("MADSIM_TEST_NUM");
