@@ -120,6 +120,7 @@ static inline uint32_t mr_kv_log_cap(uint32_t s) {
 #define MR_F_BUG_VOTE_TWICE 0x10u /* voters ignore votedFor: two leaders per term possible */
 #define MR_F_BUG_VOTE_STALE 0x20u /* voters skip the up-to-date check (Raft §5.4.1) */
 #define MR_F_BUG_NO_PREV_CHECK 0x40u /* followers skip AppendEntries' prevLogTerm check (§5.3) */
+#define MR_F_RECORD 0x80u    /* record every random draw into the batch's tape (mr_tape_get) */
 
 /* ---- verdicts: one code per tester panic site ---- */
 enum mr_fail {
@@ -201,7 +202,8 @@ typedef struct mr_cfg {
   uint32_t trace_clusters;/* with MR_F_TRACE: the first K clusters keep a trace */
   uint32_t trace_cap;     /* trace records per traced cluster */
   int32_t device;         /* HIP device ordinal */
-  uint32_t reserved[6];
+  uint32_t tape_cap;      /* with MR_F_RECORD: tape words kept per cluster (2 per draw) */
+  uint32_t reserved[5];
 } mr_cfg;
 
 /* Whole-batch counters (sums over clusters unless named max/first). */
@@ -267,6 +269,22 @@ int mr_batch_counters(mr_batch* b, mr_counters* out);
 /* Trace of traced cluster `k` (k < trace_clusters). *n = records written. */
 int mr_trace_get(mr_batch* b, uint32_t k, mr_event* out, size_t cap, size_t* n);
 void mr_batch_destroy(mr_batch* b);
+
+/* ---- decision tapes and replay (docs/SEMANTICS.md §12) ----
+ * A tape is a cluster's random draws in the order the simulation makes them, two words
+ * (w0, w1) per draw (§2). Replaying a tape makes every draw read it instead of Philox, so a
+ * recorder of another simulator's decisions (drops, latencies, timeouts, tester choices,
+ * SURVEY.md §8f rank 4) can drive the same run; draws past the end of a tape read (0, 0). */
+/* Drive cluster k of the batch from tape[k * words_per_cluster ..]; 0 words = Philox again.
+ * Call after create / reset and before run. */
+int mr_batch_set_tape(mr_batch* b, const uint32_t* tape, uint64_t words_per_cluster);
+/* The words cluster k drew so far (*n, may exceed cap or the tape) and, with MR_F_RECORD or a
+ * tape set, up to cap of them. */
+int mr_tape_get(mr_batch* b, uint32_t k, uint32_t* out, size_t cap, size_t* n);
+/* One cluster of cfg (cluster_base selects it) driven by `tape`: its per-event trace (per-node
+ * term / role / commit / applied / last / snapshot after every event) and its verdict. */
+int mr_replay(const mr_cfg* cfg, const uint32_t* tape, size_t n_words, mr_event* out, size_t cap,
+              size_t* n_out, uint16_t* code, uint32_t* time_us);
 
 #ifdef __cplusplus
 }

@@ -19,6 +19,7 @@ MR_F_SAFETY = 0x8
 MR_F_BUG_VOTE_TWICE = 0x10
 MR_F_BUG_VOTE_STALE = 0x20
 MR_F_BUG_NO_PREV_CHECK = 0x40
+MR_F_RECORD = 0x80
 
 README_SEED = 1629626496  # /root/reference/README.md:48
 
@@ -78,7 +79,7 @@ class MrCfg(C.Structure):
         ("apply_cap", C.c_uint32), ("msg_slots", C.c_uint32), ("ae_max", C.c_uint32),
         ("hb_us", C.c_uint32), ("elect_lo_us", C.c_uint32), ("elect_hi_us", C.c_uint32),
         ("max_events", C.c_uint32), ("trace_clusters", C.c_uint32), ("trace_cap", C.c_uint32),
-        ("device", C.c_int32), ("reserved", C.c_uint32 * 6),
+        ("device", C.c_int32), ("tape_cap", C.c_uint32), ("reserved", C.c_uint32 * 5),
     ]
 
 
@@ -122,5 +123,6 @@ assert EVENT_DTYPE.itemsize == 32
 EXPORTS = [
     "mr_last_error", "mr_fail_message", "mr_scenario_name", "mr_scenario_from_name",
     "mr_cfg_init", "mr_batch_create", "mr_batch_reset", "mr_batch_run", "mr_batch_verdicts",
-    "mr_batch_counters", "mr_trace_get", "mr_batch_destroy",
+    "mr_batch_counters", "mr_trace_get", "mr_batch_destroy", "mr_batch_set_tape", "mr_tape_get",
+    "mr_replay",
 ]

@@ -45,6 +45,12 @@ def _units(csrc, scns=None):
             lst = " ".join(f"MR_INST({i})" for i in ids[g::ng])
             units.append((kern, f"nb{nb}_{g}", ["-DMR_COMMON=0", f"-DMR_SCN_LIST={lst}",
                                                 f"-DMR_NB={nb}"]))
+    ids = list(scns or SCN_IDS)  # decision-tape builds (SEMANTICS §12), NB = 8
+    ng = max(1, min(N_GROUPS, (len(ids) + 3) // 4))
+    for g in range(ng):
+        lst = " ".join(f"MR_INST({i})" for i in ids[g::ng])
+        units.append((kern, f"tape_{g}", ["-DMR_COMMON=0", "-DMR_TAPE=1", f"-DMR_SCN_LIST={lst}",
+                                          "-DMR_NB=8"]))
     host = ["-DMR_DEV_SCNS=" + " ".join(f"MR_INST({i})" for i in scns)] if scns else []
     for src in sorted(glob.glob(os.path.join(csrc, "*.cpp"))):
         units.append((src, os.path.splitext(os.path.basename(src))[0], host))

@@ -53,6 +53,7 @@ enum : uint32_t {
   CS_CUT_END = CS_CUT + 2,
   CS_CCUT,   // clerk links cut: bit 8 (k mod 4) + j of word CS_CCUT + k / 4 = clerk host 8 + k !~ server j
   CS_CCUT_END = CS_CCUT + 6,
+  CS_TAPE,   // decision tape: words drawn so far (SEMANTICS §12)
   CS__N
 };
 // cs64 [C64__N][C]: per-cluster u64 scalars
@@ -157,6 +158,9 @@ struct Dev {
   uint32_t* kv32;   // [C][n][KVREC]        (kvraft only)
   uint32_t* kvs32;  // [C][n][KVS_W]        persisted KV snapshots (maxraftstate)
   uint32_t* kring;  // [C][KV_RING][KRW]    recent KV snapshots by index (maxraftstate)
+  uint32_t* tape;   // [C][tape_words]      decision tape (replay / record), else null
+  uint64_t tape_words;
+  uint32_t tape_mode;  // 0 Philox, 1 replay the tape, 2 Philox and record
   uint64_t* cval;   // [C][3][CHURN_VCAP]   churn clients' committed values (churn only)
   uint32_t* cidx;   // [C][3][CHURN_VCAP]   ... and the index each was seen at
   uint32_t* cfg32;  // [C][n][CFG_CAP][CFGW] shard_ctrler config stores
@@ -218,6 +222,10 @@ constexpr uint32_t nthr(uint32_t s) {
 // sized for its default server count (nb_of) and one for up to 8 servers
 template <uint32_t S, uint32_t NB>
 hipError_t launch_step_t(const Dev& D, uint32_t budget, hipStream_t s);
+// the same kernels built with decision-tape draws (MR_TAPE=1 translation units, NB = 8):
+// replay and record runs only, so the common draw path carries no tape branch
+template <uint32_t S, uint32_t NB>
+hipError_t launch_step_tape_t(const Dev& D, uint32_t budget, hipStream_t s);
 constexpr uint8_t k_default_n[] = {0, 3, 3, 7, 5, 3, 5, 3, 3, 5, 3, 3, 5, 3, 5,
                                    5, 5, 5, 5, 3, 3, 3, 3, 3, 5, 5, 5, 5, 3, 3,
                                    5, 5, 5, 5, 5, 5, 5, 3, 5, 3, 3, 5, 5, 5, 5, 5};

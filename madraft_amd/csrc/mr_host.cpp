@@ -20,8 +20,9 @@ hipError_t launch_step(const Dev& D, uint32_t scn, uint32_t budget, hipStream_t 
   switch (scn) {
 #define MR_INST(S)                                                                  \
   case S:                                                                           \
-    return D.n <= nb_of(S) ? launch_step_t<S, nb_of(S)>(D, budget, s)              \
-                           : launch_step_t<S, MR_MAX_NODES>(D, budget, s);
+    return D.tape_mode ? launch_step_tape_t<S, MR_MAX_NODES>(D, budget, s)          \
+           : D.n <= nb_of(S) ? launch_step_t<S, nb_of(S)>(D, budget, s)             \
+                             : launch_step_t<S, MR_MAX_NODES>(D, budget, s);
 #ifdef MR_DEV_SCNS  // dev variants built for a few scenarios (build.py scns=)
     MR_DEV_SCNS
 #else
@@ -85,6 +86,7 @@ struct mr_batch {
   hipStream_t stream = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   uint32_t budget = 16384;  // events per cluster per launch (MR_STEP_BUDGET)
+  uint32_t* tape = nullptr;  // decision tape (own allocation: set_tape / MR_F_RECORD)
 };
 
 extern "C" {
@@ -203,6 +205,8 @@ static int validate(const mr_cfg* c) {
   if (c->max_events == 0) return set_err("max_events must be > 0");
   if ((c->flags & MR_F_TRACE) && (c->trace_cap == 0 || c->trace_clusters > c->n_clusters))
     return set_err("bad trace config");
+  if ((c->flags & MR_F_RECORD) && (c->tape_cap < 2 || (c->tape_cap & 1u)))
+    return set_err("MR_F_RECORD needs an even tape_cap >= 2");
   return 0;
 }
 
@@ -295,6 +299,16 @@ int mr_batch_create(const mr_cfg* cfg, mr_batch** out) {
   for (auto& it : items) {
     *it.p = it.bytes ? p : nullptr;
     p += (it.bytes + 255) & ~size_t(255);
+  }
+  if (cfg->flags & MR_F_RECORD) {
+    e = hipMalloc(&b->tape, (size_t)C * cfg->tape_cap * sizeof(uint32_t));
+    if (e != hipSuccess) {
+      mr_batch_destroy(b);
+      return set_err(std::string("tape allocation failed: ") + hipGetErrorString(e));
+    }
+    b->D.tape = b->tape;
+    b->D.tape_words = cfg->tape_cap;
+    b->D.tape_mode = 2;
   }
   if (hipMemset(b->D.prof, 0, PROF_SLOTS * sizeof(unsigned long long)) != hipSuccess) {
     mr_batch_destroy(b);
@@ -438,6 +452,67 @@ int mr_trace_get(mr_batch* b, uint32_t k, mr_event* out, size_t cap, size_t* n) 
   return 0;
 }
 
+int mr_batch_set_tape(mr_batch* b, const uint32_t* tape, uint64_t words_per_cluster) {
+  if (!b) return set_err("null batch");
+  if (words_per_cluster && !tape) return set_err("null tape");
+  if (words_per_cluster & 1u) return set_err("tape words per cluster must be even");
+  HIPCHK(hipSetDevice(b->cfg.device));
+  HIPCHK(hipStreamSynchronize(b->stream));
+  if (b->tape) { HIPCHK(hipFree(b->tape)); b->tape = nullptr; }
+  b->D.tape = nullptr; b->D.tape_words = 0; b->D.tape_mode = 0;
+  if (!words_per_cluster) return 0;
+  const size_t bytes = (size_t)b->D.C * words_per_cluster * sizeof(uint32_t);
+  HIPCHK(hipMalloc(&b->tape, bytes));
+  HIPCHK(hipMemcpy(b->tape, tape, bytes, hipMemcpyHostToDevice));
+  b->D.tape = b->tape;
+  b->D.tape_words = words_per_cluster;
+  b->D.tape_mode = 1;
+  return 0;
+}
+
+int mr_tape_get(mr_batch* b, uint32_t k, uint32_t* out, size_t cap, size_t* n) {
+  if (!b || !n) return set_err("null argument");
+  if (k >= b->D.C) return set_err("cluster out of range");
+  HIPCHK(hipSetDevice(b->cfg.device));
+  HIPCHK(hipStreamSynchronize(b->stream));
+  uint32_t used = 0;
+  HIPCHK(hipMemcpy(&used, b->D.cs32 + (size_t)CS_TAPE * b->D.C + k, 4, hipMemcpyDeviceToHost));
+  *n = used;
+  if (!b->tape || !out) return 0;
+  size_t m = used < b->D.tape_words ? used : b->D.tape_words;
+  if (m > cap) m = cap;
+  HIPCHK(hipMemcpy(out, b->tape + (size_t)k * b->D.tape_words, m * sizeof(uint32_t),
+                   hipMemcpyDeviceToHost));
+  return 0;
+}
+
+int mr_replay(const mr_cfg* cfg, const uint32_t* tape, size_t n_words, mr_event* out, size_t cap,
+              size_t* n_out, uint16_t* code, uint32_t* time_us) {
+  if (!cfg || !n_out) return set_err("null argument");
+  if (n_words & 1u) return set_err("tape length must be even");
+  mr_cfg c = *cfg;
+  c.n_clusters = 1;
+  c.flags = (c.flags | MR_F_TRACE) & ~MR_F_RECORD;
+  c.trace_clusters = 1;
+  c.trace_cap = cap ? (uint32_t)cap : 1u;
+  mr_batch* b = nullptr;
+  int rc = mr_batch_create(&c, &b);
+  if (rc) return rc;
+  std::vector<uint32_t> pad(tape ? 0 : 2, 0u);  // an empty tape: every draw reads (0, 0)
+  rc = mr_batch_set_tape(b, tape ? tape : pad.data(), tape ? n_words : 2);
+  mr_run_stats st;
+  if (!rc) rc = mr_batch_run(b, 0, &st);
+  uint16_t cd = 0;
+  uint32_t t = 0;
+  if (!rc) rc = mr_batch_verdicts(b, &cd, &t, nullptr);
+  if (!rc && out && cap) rc = mr_trace_get(b, 0, out, cap, n_out);
+  else if (!rc) *n_out = 0;
+  if (!rc && code) *code = cd;
+  if (!rc && time_us) *time_us = t;
+  mr_batch_destroy(b);
+  return rc;
+}
+
 void mr_batch_destroy(mr_batch* b) {
   if (!b) return;
   (void)hipSetDevice(b->cfg.device);
@@ -453,6 +528,7 @@ void mr_batch_destroy(mr_batch* b) {
   }
 #endif
   if (b->base) (void)hipFree(b->base);
+  if (b->tape) (void)hipFree(b->tape);
   if (b->red) (void)hipFree(b->red);
   if (b->h_remaining) (void)hipHostFree(b->h_remaining);
   if (b->ev0) (void)hipEventDestroy(b->ev0);

@@ -23,6 +23,14 @@
 
 #include "mr_dev.h"
 
+#ifndef MR_TAPE
+#define MR_TAPE 0
+#endif
+#if MR_TAPE  // a decision-tape build of the same kernels (SEMANTICS §12): distinct symbols
+#define step_kernel step_kernel_tape
+#define launch_step_t launch_step_tape_t
+#endif
+
 namespace mr {
 
 // internal linkage: this file is compiled several times with different MR_NB
@@ -163,11 +171,30 @@ __device__ __forceinline__ uint2 philox2(uint32_t c0, uint32_t c1, uint32_t c2, 
   }
   return make_uint2(c0, c1);
 }
-// the cluster's draw: key = its seed (SEMANTICS §2)
-DI void philox(const Dev& D, const X& x, uint32_t c0, uint32_t c1, uint32_t c2, uint32_t& w0,
+// the cluster's draw: key = its seed (SEMANTICS §2); in MR_TAPE builds, with a tape set,
+// replay reads the next two words ((0, 0) past the end) and record appends the draw (§12)
+DI void philox(const Dev& D, X& x, uint32_t c0, uint32_t c1, uint32_t c2, uint32_t& w0,
                uint32_t& w1) {
-  uint64_t seed = D.seed0 + x.c;
-  uint2 w = philox2(c0, c1, c2, (uint32_t)seed, (uint32_t)(seed >> 32));
+  if constexpr (MR_TAPE) {
+    if (D.tape_mode) {
+      const uint32_t p = CS(CS_TAPE);
+      CS(CS_TAPE) = p + 2u;
+      uint32_t* tp = D.tape + (size_t)x.c * D.tape_words;
+      if (D.tape_mode == 1u) {
+        w0 = p < D.tape_words ? tp[p] : 0u;
+        w1 = p + 1u < D.tape_words ? tp[p + 1] : 0u;
+        return;
+      }
+      const uint64_t seed = D.seed0 + x.c;
+      const uint2 w = philox2(c0, c1, c2, (uint32_t)seed, (uint32_t)(seed >> 32));
+      w0 = w.x;
+      w1 = w.y;
+      if (p + 1u < D.tape_words) { tp[p] = w0; tp[p + 1] = w1; }
+      return;
+    }
+  }
+  const uint64_t seed = D.seed0 + x.c;
+  const uint2 w = philox2(c0, c1, c2, (uint32_t)seed, (uint32_t)(seed >> 32));
   w0 = w.x;
   w1 = w.y;
 }
@@ -312,8 +339,12 @@ DI int net_send(const Dev& D, X& x, uint32_t src, uint32_t& nctr, uint32_t dst, 
                 uint32_t k) {
   uint32_t seq = x.msgs_sent++;
   uint32_t ctr = nctr++;
-  if (!bit(x.conn, src) || !bit(x.conn, dst) || link_cut(D, x, src, dst)) { CADD(CNT_DROP_CLOG, 1u); return -1; }
   uint32_t w0, w1;
+  if (!bit(x.conn, src) || !bit(x.conn, dst) || link_cut(D, x, src, dst)) {
+    if (MR_TAPE && D.tape_mode) philox(D, x, ctr, src, ST_NET, w0, w1);  // its (unused) draw is on the tape
+    CADD(CNT_DROP_CLOG, 1u);
+    return -1;
+  }
   philox(D, x, ctr, src, ST_NET, w0, w1);
   if (w0 < net_loss(x)) { CADD(CNT_DROP_LOSS, 1u); return -1; }
   if (x.inflight >= D.M) { CADD(CNT_DROP_OVERFLOW, 1u); return -1; }

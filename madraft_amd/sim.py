@@ -46,6 +46,10 @@ def lib():
     L.mr_batch_counters.argtypes = [C.c_void_p, C.POINTER(MrCounters)]
     L.mr_trace_get.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_size_t,
                                C.POINTER(C.c_size_t)]
+    L.mr_batch_set_tape.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64]
+    L.mr_tape_get.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_size_t, C.POINTER(C.c_size_t)]
+    L.mr_replay.argtypes = [C.POINTER(MrCfg), C.c_void_p, C.c_size_t, C.c_void_p, C.c_size_t,
+                            C.POINTER(C.c_size_t), C.POINTER(C.c_uint16), C.POINTER(C.c_uint32)]
     L.mr_batch_destroy.argtypes = [C.c_void_p]
     L.mr_batch_destroy.restype = None
     _lib = L
@@ -148,12 +152,41 @@ class Batch:
         _check(lib().mr_batch_counters(self._b, C.byref(c)))
         return c.to_dict()
 
+    def set_tape(self, tape):
+        """Drive cluster k from tape[k] (uint32 [clusters, words], 2 words per draw;
+        SEMANTICS §12); None = Philox again. Call before run()."""
+        if tape is None:
+            _check(lib().mr_batch_set_tape(self._b, None, 0))
+            return
+        t = np.ascontiguousarray(tape, dtype=np.uint32)
+        assert t.ndim == 2 and t.shape[0] == self.clusters, t.shape
+        _check(lib().mr_batch_set_tape(self._b, t.ctypes.data, t.shape[1]))
+
+    def tape(self, k, cap=1 << 20):
+        """(words drawn by cluster k, the recorded / replayed words kept, up to cap)."""
+        out = np.empty(cap, np.uint32)
+        n = C.c_size_t()
+        _check(lib().mr_tape_get(self._b, int(k), out.ctypes.data, cap, C.byref(n)))
+        return int(n.value), out[: min(n.value, cap)]
+
     def trace(self, k, cap=None):
         cap = cap or int(self.cfg.trace_cap)
         out = np.empty(cap, EVENT_DTYPE)
         n = C.c_size_t()
         _check(lib().mr_trace_get(self._b, int(k), out.ctypes.data, cap, C.byref(n)))
         return out[: n.value]
+
+
+def replay(test, tape, trace_cap=1 << 16, cluster_base=0, **kw):
+    """mr_replay: one cluster of `test` driven by `tape` (uint32 words, 2 per draw):
+    (per-event trace, verdict code, verdict time)."""
+    cfg = make_cfg(test, 1, cluster_base=cluster_base, **kw)
+    t = np.ascontiguousarray(tape, dtype=np.uint32)
+    out = np.empty(trace_cap, EVENT_DTYPE)
+    n, code, tm = C.c_size_t(), C.c_uint16(), C.c_uint32()
+    _check(lib().mr_replay(C.byref(cfg), t.ctypes.data, t.size, out.ctypes.data, trace_cap,
+                           C.byref(n), C.byref(code), C.byref(tm)))
+    return out[: n.value], int(code.value), int(tm.value)
 
 
 def run_test(test, seed=None, num=None, **kw):

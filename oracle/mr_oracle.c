@@ -64,6 +64,11 @@ enum { CT_QUERY = 0, CT_JOIN = 1, CT_LEAVE = 2, CT_MOVE = 3 };
 #define INF_T 0xFFFFFFFFu
 #define LOSS_Q32 429496729u /* floor(0.1 * 2^32), tester.rs:130 */
 
+/* decision tapes (SEMANTICS §12): mode 1 replays, 2 records; set by mro_set_tape */
+static uint32_t* g_tape;
+static uint64_t g_tape_words, *g_tape_used;
+static int g_tape_mode;
+
 static inline uint32_t u_range(uint32_t w, uint32_t lo, uint32_t hi) {
   return lo + (uint32_t)(((uint64_t)w * (uint64_t)(hi - lo)) >> 32);
 }
@@ -144,6 +149,7 @@ typedef struct {
   uint32_t ctrl_mode, nops, ncfg[MR_MAX_NODES];
   uint32_t lring[32]; /* MR_F_SAFETY: (term << 4) | leader + 1 by term mod 32 */
   uint8_t link[MR_MAX_NODES]; /* server links (connect2/disconnect2): bit j of link[i] = i~j */
+  uint32_t* tape_row; uint64_t tape_pos; /* decision tape of this cluster (SEMANTICS §12) */
   uint8_t ccut[CK_SLOTS];     /* clerk links cut: bit j of ccut[k] = clerk host 8 + k !~ server j */
   OCfg* cfgs; /* [MR_MAX_NODES][CFG_CAP] */
   OOp* ops;   /* [OP_CAP] */
@@ -236,11 +242,28 @@ static void set_timer(OSim* s, uint32_t d, uint32_t t) {
   heap_push(s, ((uint64_t)t << 32) | (1ull << 30) | d, d, x->timer_gen);
 }
 
+/* every random draw of the simulation: Philox4x32-10 keyed by the seed (§2), or the tape */
+static void draw(OSim* s, const uint32_t ctr[4], uint32_t w[4]) {
+  uint64_t p = s->tape_pos;
+  if (s->tape_row && g_tape_mode == 1) {
+    s->tape_pos = p + 2;
+    w[0] = p < g_tape_words ? s->tape_row[p] : 0u;
+    w[1] = p + 1 < g_tape_words ? s->tape_row[p + 1] : 0u;
+    w[2] = w[3] = 0;
+    return;
+  }
+  mro_philox4x32_10(ctr, s->key, w);
+  if (s->tape_row && g_tape_mode == 2) {
+    s->tape_pos = p + 2;
+    if (p + 1 < g_tape_words) { s->tape_row[p] = w[0]; s->tape_row[p + 1] = w[1]; }
+  }
+}
+
 /* raft.rs:260-263 generate_election_timeout: U[150,300) ms */
 static void reset_timer(OSim* s, uint32_t d) {
   ONode* x = &s->nd[d];
   uint32_t ctr[4] = {x->e_ctr++, d, ST_ELECT, 0}, w[4];
-  mro_philox4x32_10(ctr, s->key, w);
+  draw(s, ctr, w);
   set_timer(s, d, s->now + u_range(w[0], s->cfg.elect_lo_us, s->cfg.elect_hi_us));
 }
 
@@ -265,7 +288,7 @@ static void net_send(OSim* s, uint32_t src, uint32_t dst, OMsg* m) {
   uint32_t seq = (uint32_t)s->r.msgs_sent;
   s->r.msgs_sent++;
   uint32_t ctr[4] = {(*host_nctr(s, src))++, src, ST_NET, 0}, w[4];
-  mro_philox4x32_10(ctr, s->key, w);
+  draw(s, ctr, w);
   if (!host_conn(s, src) || !host_conn(s, dst) || !link_up(s, src, dst)) { s->r.drop_clog++; return; }
   if (w[0] < s->loss) { s->r.drop_loss++; return; }
   if (s->inflight >= s->cfg.msg_slots) { s->r.drop_overflow++; return; }
@@ -874,7 +897,7 @@ static void t_sleep(OSim* s, uint32_t us) { /* time::sleep */
 
 static void t_draw(OSim* s, uint32_t w[4]) {
   uint32_t ctr[4] = {s->t_ctr++, 0, ST_TESTER, 0};
-  mro_philox4x32_10(ctr, s->key, w);
+  draw(s, ctr, w);
 }
 static uint32_t t_range(OSim* s, uint32_t lo, uint32_t hi) {
   uint32_t w[4]; t_draw(s, w); return u_range(w[0], lo, hi);
@@ -1452,7 +1475,7 @@ static int clerk_resume(OSim* s, uint32_t slot) {
 
 static int thr_bool(OSim* s, OThr* t, uint32_t p_q32) { /* rng.gen_bool on the thread's stream */
   uint32_t ctr[4] = {t->tctr++, t->tid, ST_TESTER, 0}, w[4];
-  mro_philox4x32_10(ctr, s->key, w);
+  draw(s, ctr, w);
   return w[0] < p_q32;
 }
 
@@ -1525,7 +1548,7 @@ static void t_connect_all(OSim* s) { memset(s->link, 0xFF, sizeof s->link); } /*
 
 static uint32_t thr_range(OSim* s, OThr* t, uint32_t lo, uint32_t hi) { /* rng.gen_range(lo..hi) */
   uint32_t ctr[4] = {t->tctr++, t->tid, ST_TESTER, 0}, w[4];
-  mro_philox4x32_10(ctr, s->key, w);
+  draw(s, ctr, w);
   return u_range(w[0], lo, hi);
 }
 
@@ -1560,7 +1583,7 @@ static void part_step(OSim* s, uint32_t slot) {
 /* ---- raft tests with spawn_local (tests.rs:662-686, 743-856) ---- */
 static uint64_t thr_entry(OSim* s, OThr* t) { /* random.gen_entry() on the thread's stream */
   uint32_t ctr[4] = {t->tctr++, t->tid, ST_TESTER, 0}, w[4];
-  mro_philox4x32_10(ctr, s->key, w);
+  draw(s, ctr, w);
   return ((uint64_t)w[1] << 32) | w[0];
 }
 
@@ -2341,6 +2364,9 @@ static void sim_reset(OSim* s, uint64_t cluster) {
   memset(&s->r, 0, sizeof s->r);
   s->r.digest = 0xCBF29CE484222325ull;
   s->n_trace = 0;
+  uint64_t row = cluster - s->cfg.cluster_base;
+  s->tape_row = g_tape_mode ? g_tape + row * g_tape_words : NULL;
+  s->tape_pos = 0;
 }
 
 static void sim_run(OSim* s, uint64_t cluster) {
@@ -2350,6 +2376,11 @@ static void sim_run(OSim* s, uint64_t cluster) {
     s->r.ev_tester++;
     if (run_scenario(s) != 0) t_fail(s, MR_FAIL_SIM_BAD_PROGRAM);
   }
+  if (g_tape_mode && g_tape_used) g_tape_used[cluster - s->cfg.cluster_base] = s->tape_pos;
+}
+
+void mro_set_tape(uint32_t* tape, uint64_t words_per_cluster, int mode, uint64_t* used) {
+  g_tape = tape; g_tape_words = words_per_cluster; g_tape_mode = tape ? mode : 0; g_tape_used = used;
 }
 
 int mro_run_cluster(const mr_cfg* cfg, uint64_t cluster, mro_result* out, mr_event* trace,

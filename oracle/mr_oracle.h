@@ -46,6 +46,11 @@ int mro_run_batch(const mr_cfg* cfg, uint64_t first, uint64_t count,
                   uint16_t* code, uint32_t* time_us, uint64_t* digest,
                   mro_result* sum);
 
+/* Decision tapes (SEMANTICS §12) for the following runs: mode 1 replays tape row
+ * (cluster - cfg.cluster_base), mode 2 records into it; used[row] = words drawn. NULL = off.
+ * Not thread-safe (one tape per process). */
+void mro_set_tape(uint32_t* tape, uint64_t words_per_cluster, int mode, uint64_t* used);
+
 /* Philox4x32-10 block (exported for the known-answer test). */
 void mro_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]);
 

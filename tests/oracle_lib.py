@@ -40,6 +40,8 @@ class Oracle:
                                         C.POINTER(C.c_uint32 * 4)]
         L.mro_philox4x32_10.restype = None
         L.mro_cfg_init.argtypes = [C.POINTER(MrCfg), C.c_uint32]
+        L.mro_set_tape.argtypes = [C.c_void_p, C.c_uint64, C.c_int, C.c_void_p]
+        L.mro_set_tape.restype = None
         L.mro_scenario_from_name.argtypes = [C.c_char_p]
         L.mro_scenario_from_name.restype = C.c_uint32
         self.L = L
@@ -72,6 +74,22 @@ class Oracle:
                                     C.byref(n))
         assert rc == 0, "bad config"
         return r.to_dict(), tr[: min(n.value, trace_cap)] if trace_cap else None
+
+    def with_tape(self, tape, mode):
+        """Context: the following runs replay (mode 1) or record into (mode 2) `tape`
+        (uint32 [clusters, words], row = cluster - cfg.cluster_base); yields words drawn."""
+        import contextlib
+
+        @contextlib.contextmanager
+        def ctx():
+            used = np.zeros(tape.shape[0], np.uint64)
+            self.L.mro_set_tape(tape.ctypes.data, tape.shape[1], mode, used.ctypes.data)
+            try:
+                yield used
+            finally:
+                self.L.mro_set_tape(None, 0, 0, None)
+        assert tape.dtype == np.uint32 and tape.flags.c_contiguous
+        return ctx()
 
     def run_batch(self, cfg, first, count):
         code = np.empty(count, np.uint16)
