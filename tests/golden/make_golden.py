@@ -24,6 +24,14 @@ CASES += [
          count=16),
     dict(test="snapshot_install_unreliable_2d", cfg={"n_nodes": 7}, first=0, count=8),
     dict(test="figure_8_unreliable_2c", cfg={}, first=1000, count=16),
+    # Raft invariant checks and the buggy variants they catch (SEMANTICS §11)
+    dict(test="figure_8_unreliable_2c", cfg={"flags": _abi.MR_F_SAFETY}, first=0, count=8),
+    dict(test="many_election_2a", cfg={"flags": _abi.MR_F_SAFETY | _abi.MR_F_BUG_VOTE_TWICE},
+         first=0, count=16),
+    dict(test="figure_8_2c", cfg={"flags": _abi.MR_F_SAFETY | _abi.MR_F_BUG_VOTE_STALE},
+         first=0, count=8),
+    dict(test="rejoin_2b", cfg={"flags": _abi.MR_F_SAFETY | _abi.MR_F_BUG_NO_PREV_CHECK},
+         first=0, count=8),
 ]
 
 
