@@ -226,6 +226,9 @@ typedef struct mr_counters {
   /* coverage histograms over clusters, bucket b = 0 for 0, else min(15, 1 + floor(log2 v)) */
   uint64_t cov_leaders[16]; /* leaders elected per cluster */
   uint64_t cov_events[16];  /* events per cluster */
+  /* services (kvraft / shard_ctrler; BASELINE config 5 "linearizability-check counters") */
+  uint64_t kv_ops;          /* clerk calls completed */
+  uint64_t kv_checked;      /* Get results the tester verified against their linearizable value */
 } mr_counters;
 
 typedef struct mr_run_stats {

@@ -90,7 +90,8 @@ class MrCounters(C.Structure):
         "elections", "leaders_elected", "applies", "snapshots", "installs", "entries_shipped",
         "virt_time_us", "max_inflight", "max_log", "max_index", "first_fail_cluster",
         "first_fail_code")] + [("fail_hist", C.c_uint64 * 64), ("cov_leaders", C.c_uint64 * 16),
-                               ("cov_events", C.c_uint64 * 16)]
+                               ("cov_events", C.c_uint64 * 16), ("kv_ops", C.c_uint64),
+                               ("kv_checked", C.c_uint64)]
 
     def to_dict(self):
         d = {n: getattr(self, n) for n, _ in self._fields_

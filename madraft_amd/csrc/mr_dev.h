@@ -54,6 +54,7 @@ enum : uint32_t {
   CS_CCUT,   // clerk links cut: bit 8 (k mod 4) + j of word CS_CCUT + k / 4 = clerk host 8 + k !~ server j
   CS_CCUT_END = CS_CCUT + 6,
   CS_TAPE,   // decision tape: words drawn so far (SEMANTICS §12)
+  CS_KV_OPS, CS_KV_CHECKED,  // service clerk calls completed / Get results verified
   CS__N
 };
 // cs64 [C64__N][C]: per-cluster u64 scalars

@@ -73,7 +73,7 @@ const uint8_t k_nodes[MR_SCN_COUNT_] = {0, 3, 3, 7, 5, 3, 5, 3, 3, 5, 3, 3, 5, 3
                                         5, 5, 5, 5, 5, 3, 3, 3, 3, 3, 5, 5, 5, 5, 3, 3,
                                         5, 5, 5, 5, 5, 5, 5, 3, 5, 3, 3, 5, 5, 5, 5, 5};
 
-constexpr size_t RED_N = CNT__N + 8 + 64 + 32;  // reduce_kernel output slots
+constexpr size_t RED_N = CNT__N + 8 + 64 + 32 + 2;  // reduce_kernel output slots
 }  // namespace
 
 struct mr_batch {
@@ -428,6 +428,8 @@ int mr_batch_counters(mr_batch* b, mr_counters* out) {
     out->cov_leaders[i] = h[CNT__N + 72 + i];
     out->cov_events[i] = h[CNT__N + 88 + i];
   }
+  out->kv_ops = h[CNT__N + 104];
+  out->kv_checked = h[CNT__N + 105];
   out->first_fail_code = 0;
   if (out->first_fail_cluster != ~0ull) {
     uint32_t code = 0;

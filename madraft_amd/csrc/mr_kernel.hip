@@ -1224,7 +1224,7 @@ __global__ void __launch_bounds__(256) reset_kernel(Dev D) {
 // cluster; out[] layout documented in mr_host.cpp (RED_*)
 __global__ void __launch_bounds__(256) reduce_kernel(Dev D, unsigned long long* out,
                                                     uint64_t cluster_base) {
-  constexpr uint32_t RN = CNT__N + 8 + 64 + 32;  // counters, scalars, verdicts, coverage
+  constexpr uint32_t RN = CNT__N + 8 + 64 + 32 + 2;  // counters, scalars, verdicts, coverage, kv
   __shared__ unsigned long long acc[RN];
   for (uint32_t i = threadIdx.x; i < RN; i += blockDim.x) acc[i] = 0;
   __syncthreads();
@@ -1246,6 +1246,8 @@ __global__ void __launch_bounds__(256) reduce_kernel(Dev D, unsigned long long* 
     auto bucket = [](uint32_t v) { return v == 0 ? 0u : min(15u, 32u - (uint32_t)__builtin_clz(v)); };
     atomicAdd(&acc[CNT__N + 72 + bucket(CS(CS_CNT + CNT_LEADERS))], 1ull);
     atomicAdd(&acc[CNT__N + 88 + bucket(CS(CS_EVENTS))], 1ull);
+    atomicAdd(&acc[CNT__N + 104], (unsigned long long)CS(CS_KV_OPS));
+    atomicAdd(&acc[CNT__N + 105], (unsigned long long)CS(CS_KV_CHECKED));
     if (code != RUN && code != MR_PASS)
       atomicMin(&out[CNT__N + 5], (unsigned long long)(cluster_base + x.c));
   }

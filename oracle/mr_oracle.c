@@ -1464,7 +1464,7 @@ static int clerk_resume(OSim* s, uint32_t slot) {
   OClerk* c = &s->ck[slot];
   c->waiting = 0;
   if (c->got) {
-    if (c->rstat == KV_OK) return 1;
+    if (c->rstat == KV_OK) { s->r.kv_ops++; return 1; }
     c->lh = c->rstat == KV_WRONG_LEADER ? c->rhint : (c->lh + 1) % s->n;
   } else {
     c->lh = (c->lh + 1) % s->n;
@@ -1513,6 +1513,7 @@ static void kv_client_step(OSim* s, uint32_t slot) {
       case 3: if (!clerk_resume(s, slot)) goto block; t->j++; t->pc = 2; break;
       case 4:
         if (!clerk_resume(s, slot)) goto block;
+        s->r.kv_checked++;
         if (c->rvh != t->hlast) t_fail(s, MR_FAIL_KV_GET_WRONG); /* kvraft/tests.rs:127 */
         t->pc = 2;
         break;
@@ -1812,6 +1813,7 @@ static void main_clerk(OSim* s, uint32_t k, uint32_t id, uint32_t to) {
 static void t_connect_client(OSim* s, uint32_t k, uint32_t to) { s->ccut[k] = (uint8_t)~to; }
 static void t_check(OSim* s, uint32_t k, uint32_t key, uint32_t tok) { /* Clerk::check */
   main_callk(s, k, KV_GET, key, 0);
+  s->r.kv_checked++;
   if (s->ck[k].rvh != put_hash(tok)) t_fail(s, MR_FAIL_KV_CHECK);
 }
 static uint32_t kv_leader(OSim* s) { /* Tester::leader (kvraft/tester.rs:171-182) */
@@ -1864,6 +1866,7 @@ static void scn_kv_one_key(OSim* s) { /* unreliable_one_key_3a, kvraft/tests.rs:
   }
   t_join_all(s);
   uint32_t v = main_call(s, KV_GET, K, KV_ALL);
+  s->r.kv_checked++;
   for (uint32_t i = 0; i < 5; i++) { /* check_concurrent_appends(&vx, &counts) */
     uint32_t f = (v >> (6 * i)) & 63u;
     if (!(f >> 5)) t_fail(s, MR_FAIL_KV_APPEND_BAD);
@@ -2010,6 +2013,7 @@ static void scn_kv_generic(OSim* s, uint32_t nclients, int unreliable, int crash
       t_join(s, 1 + cli);
       uint32_t j = s->th[1 + cli].j;
       uint32_t v = main_call(s, KV_GET, cli, cli); /* check_clnt_appends(cli, &v, j) */
+      s->r.kv_checked++;
       if (!(v >> 31)) t_fail(s, MR_FAIL_KV_APPEND_BAD);         /* kvraft/tests.rs:31-39 */
       if ((v & 0x7FFFFFFFu) < j) t_fail(s, MR_FAIL_KV_MISSING); /* kvraft/tests.rs:25-30 */
     }
@@ -2407,6 +2411,7 @@ static void acc(mro_result* a, const mro_result* b) {
   if (b->max_inflight > a->max_inflight) a->max_inflight = b->max_inflight;
   if (b->max_log > a->max_log) a->max_log = b->max_log;
   if (b->max_index > a->max_index) a->max_index = b->max_index;
+  a->kv_ops += b->kv_ops; a->kv_checked += b->kv_checked;
 }
 
 int mro_run_batch(const mr_cfg* cfg, uint64_t first, uint64_t count, uint16_t* code,

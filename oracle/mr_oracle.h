@@ -34,6 +34,8 @@ typedef struct mro_result {
   uint64_t msgs_sent, drop_clog, drop_loss, drop_overflow, drop_deliver, drop_stale;
   uint64_t elections, leaders_elected, applies, snapshots, installs, entries_shipped;
   uint64_t max_inflight, max_log, max_index;
+  uint64_t kv_ops;      /* service clerk calls completed (kvraft / shard_ctrler) */
+  uint64_t kv_checked;  /* Get results the tester verified against their linearizable value */
 } mro_result;
 
 /* Run cluster `cluster` (global id) of cfg; trace (optional) receives up to

@@ -20,7 +20,7 @@ SUPPORTED = [n for n in _abi.SCENARIOS if n and n not in _abi.GPU_UNSUPPORTED]
 COUNTER_KEYS = ["events", "ev_msg", "ev_timer", "ev_tester", "msgs_sent", "drop_clog",
                 "drop_loss", "drop_overflow", "drop_deliver", "drop_stale", "elections",
                 "leaders_elected", "applies", "snapshots", "installs", "entries_shipped",
-                "max_inflight", "max_log", "max_index"]
+                "max_inflight", "max_log", "max_index", "kv_ops", "kv_checked"]
 
 
 def first_diff(a, b):
