@@ -79,6 +79,15 @@ def test_snapshot_7_nodes(hip, oracle):
     assert cnt["installs"] > 0 and cnt["snapshots"] > 0
 
 
+@pytest.mark.parametrize("test", ["figure_8_unreliable_2c", "many_partitions_many_clients_3a",
+                                  "snapshot_unreliable_3b", "unreliable_churn_2c"])
+def test_eight_servers(hip, oracle, test):
+    """MR_MAX_NODES = 8 servers (the NB = 8 kernel instances) on scenarios built for 5."""
+    kw = {"iters": 200} if test == "figure_8_unreliable_2c" else {}
+    # a few 8-server partition runs never settle: the event cap ends them alike on both sides
+    compare(hip, oracle, test, 128, traced=2, nodes=8, max_events=200000, **kw)
+
+
 def test_kv_unreliable_traced(hip, oracle):
     """BASELINE config 5 shape: 5 servers + 5 clerk threads over the unreliable
     net; traced clusters compared record by record (clerk deliveries, client
