@@ -4,7 +4,7 @@ import argparse
 import json
 import time
 
-from . import sim
+from . import _abi, sim
 
 
 def main():
@@ -16,10 +16,19 @@ def main():
     ap.add_argument("--iters", type=int, default=0)
     ap.add_argument("--unreliable", action="store_true")
     ap.add_argument("--null", action="store_true", help="skeleton node (never campaigns)")
+    ap.add_argument("--safety", action="store_true",
+                    help="per-event Raft invariant checks (docs/SEMANTICS.md §11)")
+    ap.add_argument("--bug", choices=["vote_twice", "vote_stale", "no_prev_check"],
+                    help="run a known-buggy Raft variant")
     a = ap.parse_args()
+    flags = 0
+    if a.bug:
+        flags |= {"vote_twice": _abi.MR_F_BUG_VOTE_TWICE, "vote_stale": _abi.MR_F_BUG_VOTE_STALE,
+                  "no_prev_check": _abi.MR_F_BUG_NO_PREV_CHECK}[a.bug]
     t0 = time.time()
     code, _, _, cnt = sim.run_test(a.test, a.seed, a.clusters, nodes=a.nodes, iters=a.iters,
-                                   unreliable=a.unreliable, null_raft=a.null)
+                                   unreliable=a.unreliable, null_raft=a.null, safety=a.safety,
+                                   flags=flags)
     cnt["wall_s"] = time.time() - t0
     print(json.dumps(cnt))
     raise SystemExit(0 if cnt["failed"] == 0 else 1)
