@@ -266,6 +266,14 @@ int mr_batch_reset(mr_batch* b, uint64_t seed_base);
 /* Run until every cluster has a verdict or max_events_per_call events per
  * cluster were processed in this call (0 = no per-call bound). */
 int mr_batch_run(mr_batch* b, uint64_t max_events_per_call, mr_run_stats* st);
+/* Pipelined steps (the benchmark's double-buffered batches): mr_batch_submit enqueues
+ * mr_batch_reset(seed_base) and the first step-kernel launch on the batch's own stream and
+ * returns at once; mr_batch_finish waits for them, runs any clusters left past the per-launch
+ * budget to their verdict, and returns the run stats and (cnt != NULL) the counters.
+ * A second batch's step submitted meanwhile fills the CUs this batch's finished waves free.
+ * Results are those of mr_batch_reset + mr_batch_run. */
+int mr_batch_submit(mr_batch* b, uint64_t seed_base);
+int mr_batch_finish(mr_batch* b, mr_run_stats* st, mr_counters* cnt);
 /* Per-cluster verdict code, fail/end time (virtual us) and trace digest. */
 int mr_batch_verdicts(mr_batch* b, uint16_t* code, uint32_t* time_us, uint64_t* digest);
 int mr_batch_counters(mr_batch* b, mr_counters* out);

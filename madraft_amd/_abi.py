@@ -125,5 +125,5 @@ EXPORTS = [
     "mr_last_error", "mr_fail_message", "mr_scenario_name", "mr_scenario_from_name",
     "mr_cfg_init", "mr_batch_create", "mr_batch_reset", "mr_batch_run", "mr_batch_verdicts",
     "mr_batch_counters", "mr_trace_get", "mr_batch_destroy", "mr_batch_set_tape", "mr_tape_get",
-    "mr_replay",
+    "mr_replay", "mr_batch_submit", "mr_batch_finish",
 ]

@@ -87,6 +87,8 @@ struct mr_batch {
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   uint32_t budget = 16384;  // events per cluster per launch (MR_STEP_BUDGET)
   uint32_t* tape = nullptr;  // decision tape (own allocation: set_tape / MR_F_RECORD)
+  bool submitted = false;    // mr_batch_submit enqueued a step not yet finished
+  std::chrono::steady_clock::time_point t_submit;
 };
 
 extern "C" {
@@ -325,8 +327,7 @@ int mr_batch_create(const mr_cfg* cfg, mr_batch** out) {
   return 0;
 }
 
-int mr_batch_reset(mr_batch* b, uint64_t seed_base) {
-  if (!b) return set_err("null batch");
+static int enqueue_reset(mr_batch* b, uint64_t seed_base) {
   b->cfg.seed_base = seed_base;
   b->D.seed0 = seed_base + b->cfg.cluster_base;
   HIPCHK(hipSetDevice(b->cfg.device));
@@ -338,12 +339,32 @@ int mr_batch_reset(mr_batch* b, uint64_t seed_base) {
     HIPCHK(hipMemsetAsync(b->D.kring, 0, (size_t)b->D.C * KV_RING * KRW * sizeof(uint32_t), b->stream));
   }
   HIPCHK(launch_reset(b->D, b->stream));
+  return 0;
+}
+
+// one step-kernel launch on the batch stream, bracketed by the timing events;
+// the remaining-cluster count is copied back asynchronously
+static int enqueue_step(mr_batch* b, uint32_t budget) {
+  HIPCHK(hipMemsetAsync(b->D.remaining, 0, sizeof(uint32_t), b->stream));
+  HIPCHK(hipEventRecord(b->ev0, b->stream));
+  HIPCHK(launch_step(b->D, b->D.scenario, budget, b->stream));
+  HIPCHK(hipEventRecord(b->ev1, b->stream));
+  HIPCHK(hipMemcpyAsync(b->h_remaining, b->D.remaining, sizeof(uint32_t), hipMemcpyDeviceToHost,
+                        b->stream));
+  return 0;
+}
+
+int mr_batch_reset(mr_batch* b, uint64_t seed_base) {
+  if (!b) return set_err("null batch");
+  if (b->submitted) return set_err("batch has a submitted step: mr_batch_finish it first");
+  if (enqueue_reset(b, seed_base) != 0) return -1;
   HIPCHK(hipStreamSynchronize(b->stream));
   return 0;
 }
 
 int mr_batch_run(mr_batch* b, uint64_t max_events_per_call, mr_run_stats* st) {
   if (!b) return set_err("null batch");
+  if (b->submitted) return set_err("batch has a submitted step: mr_batch_finish it first");
   HIPCHK(hipSetDevice(b->cfg.device));
   auto t0 = std::chrono::steady_clock::now();
   mr_run_stats s;
@@ -356,12 +377,7 @@ int mr_batch_run(mr_batch* b, uint64_t max_events_per_call, mr_run_stats* st) {
       uint64_t left = max_events_per_call - done_events;
       if (left < budget) budget = (uint32_t)left;
     }
-    HIPCHK(hipMemsetAsync(b->D.remaining, 0, sizeof(uint32_t), b->stream));
-    HIPCHK(hipEventRecord(b->ev0, b->stream));
-    HIPCHK(launch_step(b->D, b->D.scenario, budget, b->stream));
-    HIPCHK(hipEventRecord(b->ev1, b->stream));
-    HIPCHK(hipMemcpyAsync(b->h_remaining, b->D.remaining, sizeof(uint32_t), hipMemcpyDeviceToHost,
-                          b->stream));
+    if (enqueue_step(b, budget) != 0) return -1;
     HIPCHK(hipStreamSynchronize(b->stream));
     float ms = 0.f;
     HIPCHK(hipEventElapsedTime(&ms, b->ev0, b->ev1));
@@ -377,6 +393,49 @@ int mr_batch_run(mr_batch* b, uint64_t max_events_per_call, mr_run_stats* st) {
   if (mr_batch_counters(b, &c) != 0) return -1;
   s.events = c.events;
   if (st) *st = s;
+  return 0;
+}
+
+// Pipelined steps (bench.py): reset + the first step-kernel launch are only
+// enqueued, so the host can queue the next batch's step on its own stream and
+// that batch's waves take the CUs this batch's early-finishing waves free.
+int mr_batch_submit(mr_batch* b, uint64_t seed_base) {
+  if (!b) return set_err("null batch");
+  if (b->submitted) return set_err("batch already has a submitted step");
+  b->t_submit = std::chrono::steady_clock::now();
+  if (enqueue_reset(b, seed_base) != 0) return -1;
+  if (enqueue_step(b, b->budget) != 0) return -1;
+  b->submitted = true;
+  return 0;
+}
+
+int mr_batch_finish(mr_batch* b, mr_run_stats* st, mr_counters* cnt) {
+  if (!b) return set_err("null batch");
+  if (!b->submitted) return set_err("no submitted step");
+  HIPCHK(hipSetDevice(b->cfg.device));
+  HIPCHK(hipStreamSynchronize(b->stream));
+  b->submitted = false;
+  mr_run_stats s;
+  std::memset(&s, 0, sizeof s);
+  float ms = 0.f;
+  HIPCHK(hipEventElapsedTime(&ms, b->ev0, b->ev1));
+  s.kernel_ms = ms;
+  s.launches = 1;
+  s.remaining = *b->h_remaining;
+  if (s.remaining != 0) {  // clusters past the per-launch budget: finish them synchronously
+    mr_run_stats more;
+    if (mr_batch_run(b, 0, &more) != 0) return -1;
+    s.kernel_ms += more.kernel_ms;
+    s.launches += more.launches;
+    s.remaining = more.remaining;
+  }
+  mr_counters c;
+  if (mr_batch_counters(b, &c) != 0) return -1;
+  s.events = c.events;
+  s.wall_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() -
+                                                        b->t_submit).count();
+  if (st) *st = s;
+  if (cnt) *cnt = c;
   return 0;
 }
 

@@ -42,6 +42,8 @@ def lib():
     L.mr_batch_create.argtypes = [C.POINTER(MrCfg), C.POINTER(C.c_void_p)]
     L.mr_batch_reset.argtypes = [C.c_void_p, C.c_uint64]
     L.mr_batch_run.argtypes = [C.c_void_p, C.c_uint64, C.POINTER(MrRunStats)]
+    L.mr_batch_submit.argtypes = [C.c_void_p, C.c_uint64]
+    L.mr_batch_finish.argtypes = [C.c_void_p, C.POINTER(MrRunStats), C.POINTER(MrCounters)]
     L.mr_batch_verdicts.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
     L.mr_batch_counters.argtypes = [C.c_void_p, C.POINTER(MrCounters)]
     L.mr_trace_get.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_size_t,
@@ -137,6 +139,18 @@ class Batch:
         st = MrRunStats()
         _check(lib().mr_batch_run(self._b, int(max_events), C.byref(st)))
         return {n: getattr(st, n) for n, _ in MrRunStats._fields_}
+
+    def submit(self, seed_base):
+        """reset(seed_base) + run()'s first launch, enqueued without waiting (mr_batch_submit);
+        finish() completes it. Another batch's step can be submitted in between."""
+        self.cfg.seed_base = int(seed_base)
+        _check(lib().mr_batch_submit(self._b, int(seed_base)))
+
+    def finish(self):
+        """(run stats, counters) of the submitted step (mr_batch_finish)."""
+        st, c = MrRunStats(), MrCounters()
+        _check(lib().mr_batch_finish(self._b, C.byref(st), C.byref(c)))
+        return {n: getattr(st, n) for n, _ in MrRunStats._fields_}, c.to_dict()
 
     def verdicts(self):
         n = self.clusters

@@ -43,3 +43,44 @@ def test_bench_two_ranks_one_gpu():
                 "--no-cpu-baseline"])
     # same seeds (global cluster ids), so the same events whatever the rank count
     assert d["events_per_seed"] == one["events_per_seed"]
+
+
+@pytest.mark.parametrize("budget", [None, "700"])
+def test_submit_finish_pipeline_equals_run(budget, monkeypatch):
+    """Two batches stepped as bench.py does (mr_batch_submit of step i+1 before
+    mr_batch_finish of step i, each on its own stream) give every cluster's verdict,
+    verdict time and trace digest, and the counters, of reset + run on one batch —
+    also when clusters outlive the first launch (small MR_STEP_BUDGET)."""
+    import numpy as np
+
+    from madraft_amd import _abi, sim
+    if budget:
+        monkeypatch.setenv("MR_STEP_BUDGET", budget)
+    test, n, seeds = "figure_8_unreliable_2c", 2048, [_abi.README_SEED + k * 7919 for k in range(3)]
+    kw = dict(iters=200, safety=True)
+    want = []
+    with sim.Batch(test, n, **kw) as ref:
+        for s in seeds:
+            ref.reset(s)
+            st = ref.run()
+            assert st["remaining"] == 0
+            want.append((ref.verdicts(), ref.counters()))
+    bufs = [sim.Batch(test, n, **kw), sim.Batch(test, n, **kw)]
+    try:
+        got = []
+        bufs[0].submit(seeds[0])
+        for j in range(len(seeds)):
+            if j + 1 < len(seeds):
+                bufs[(j + 1) % 2].submit(seeds[j + 1])
+            st, c = bufs[j % 2].finish()
+            assert st["remaining"] == 0 and st["launches"] >= (2 if budget else 1)
+            got.append((bufs[j % 2].verdicts(), c))
+        with pytest.raises(sim.SimError):
+            bufs[0].finish()  # nothing submitted
+    finally:
+        for b in bufs:
+            b.close()
+    for (wv, wc), (gv, gc) in zip(want, got):
+        for x, y in zip(wv, gv):
+            assert np.array_equal(x, y)
+        assert wc == gc
