@@ -30,6 +30,16 @@ def test_bench_single_rank_json():
     assert d["roofline"]["bound"] == "hbm" and 0 < d["roofline"]["frac"] < 1
 
 
+def test_bench_pipelined_steps_same_work():
+    """bench.py --pipeline (two batches, step i+1 queued while step i runs) processes the
+    same seeds, so the same events, as the default serial steps."""
+    args = [sys.executable, "bench.py", "--steps", "3", "--warmup", "1", "--clusters", "4096",
+            "--no-cpu-baseline"]
+    serial, piped = _run(args), _run(args + ["--pipeline"])
+    assert piped["events_per_seed"] == serial["events_per_seed"]
+    assert piped["pass_rate"] == serial["pass_rate"] and piped["roofline"]["launches"] == 3
+
+
 def test_bench_two_ranks_one_gpu():
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
