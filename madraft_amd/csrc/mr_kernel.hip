@@ -422,8 +422,11 @@ DI void guard_log_write(const Dev& D, X& x, uint32_t L, uint32_t& pexp, uint32_t
 #define MR_AC 8
 #endif
 constexpr uint32_t AC = MR_AC;  // entries per batch of independent loads in log walks
-#ifndef MR_AC_APPLY
-#define MR_AC_APPLY 8
+#ifndef MR_AP_PIPE  // software-pipelined applier batches (node_apply); A/B in DESIGN.md §6
+#define MR_AP_PIPE 1
+#endif
+#ifndef MR_AC_APPLY  // pipelined: two batches of 5 in flight fit the registers (8: spills)
+#define MR_AC_APPLY (MR_AP_PIPE ? 5 : 8)
 #endif
 constexpr uint32_t AC_APPLY = MR_AC_APPLY;  // entries per batch in the applier
 DI void storage_snapshot(const Dev& D, X& x, uint32_t i, uint32_t& slen, uint32_t idx) {  // tester.rs:399-402
@@ -467,6 +470,73 @@ DI void node_apply(const Dev& D, X& x, uint32_t me, NC& d, bool& kvready) {
   const bool snapmode = (x.netmode >> 1) & 1u;
   SE* const sb = D.stor + (size_t)x.c * D.apply_cap;
   uint32_t len = d.slen;
+#if MR_AP_PIPE
+  // software-pipelined: batch b + 1's loads are issued before batch b's checker stores, so
+  // they do not wait behind them on vmcnt (disjoint indices: a batch never reads what an
+  // earlier one wrote; the log is not written here)
+  LE e[AC_APPLY];
+  uint32_t m[AC_APPLY];
+  uint64_t sv[AC_APPLY];
+  auto load_batch = [&](uint32_t i0) {
+#pragma unroll
+    for (uint32_t j = 0; j < AC_APPLY; j++) {
+      const uint32_t i = i0 + j;
+      const bool ok = i <= d.commit && i < D.apply_cap;
+      e[j] = ok ? D.log[logi(D, x, me, i)] : LE{};
+      const SE s = ok ? sb[i] : SE{};
+      m[j] = s.mask;
+      sv[j] = s.val;
+    }
+  };
+  if (d.applied < d.commit) load_batch(d.applied + 1);
+  while (d.applied < d.commit) {
+    const uint32_t i0 = d.applied + 1;
+    LE ce[AC_APPLY];
+    uint32_t cm[AC_APPLY];
+    uint64_t csv[AC_APPLY];
+#pragma unroll
+    for (uint32_t j = 0; j < AC_APPLY; j++) { ce[j] = e[j]; cm[j] = m[j]; csv[j] = sv[j]; }
+    if (i0 + AC_APPLY <= d.commit) load_batch(i0 + AC_APPLY);
+    PROF(P_AP_LOAD);
+#pragma unroll
+    for (uint32_t j = 0; j < AC_APPLY; j++) {
+      const uint32_t i = i0 + j;
+      if (i > d.commit) break;
+      d.applied = i;
+      if (i >= D.apply_cap) { fail(D, x, MR_FAIL_SIM_CAPACITY); return; }
+      CADD(CNT_APPLIES, 1u);
+      if (cm[j] && csv[j] != ce[j].val) { fail(D, x, MR_FAIL_APPLY_MISMATCH); return; }  // tester.rs:384
+      if (i > len) { fail(D, x, MR_FAIL_APPLY_OUT_OF_ORDER); return; }  // tester.rs:393
+      if (i == len) {
+        sb[i] = SE{ce[j].val, cm[j] | (1u << me), 0u};
+        len++;
+        CMAX(CNT_MAX_INDEX, i);
+      }
+      if (snapmode && (i + 1) % 10u == 0 && i > d.snap) {  // 2D: service snapshots every 10
+        d.snapt = ce[j].term;
+        d.snap = i;
+        NSV(me) = ce[j].val;
+        CADD(CNT_SNAPSHOTS, 1u);
+      }
+      if constexpr (KV) {
+        kv_apply<is_ctrl(S)>(D, x, me, i, ce[j].val, kvready);
+        if (x.code != RUN) return;
+      }
+      if constexpr (kv_gen(S).maxraft > 0) {  // the KV service snapshots (SEMANTICS §9)
+        const uint32_t sz = 32u + (f_voted(d.f) != 15u ? 9u : 1u) + 24u * (d.last - d.snap);
+        if (i % KV_SNAP_EVERY == 0 && i > d.snap && sz >= kv_gen(S).maxraft / 2) {
+          d.snapt = ce[j].term;
+          d.snap = i;
+          NSV(me) = ce[j].val;
+          CADD(CNT_SNAPSHOTS, 1u);
+          kv_snapshot(D, x, me, i);
+          if (x.code != RUN) return;
+        }
+      }
+    }
+    PROF(P_AP_CHECK);
+  }
+#else
   while (d.applied < d.commit) {
     const uint32_t i0 = d.applied + 1;
     LE e[AC_APPLY];
@@ -520,6 +590,7 @@ DI void node_apply(const Dev& D, X& x, uint32_t me, NC& d, bool& kvready) {
     }
     PROF(P_AP_CHECK);
   }
+#endif
   d.slen = len;
 }
 
