@@ -378,10 +378,15 @@ DI int net_send(const Dev& D, X& x, uint32_t src, uint32_t& nctr, uint32_t dst, 
 constexpr uint32_t HDR_MAT = 1u << 28;  // message header: payload copied into D.pay
 constexpr uint32_t LAT_BOUND_US = 27000u;
 
-DI void pend_note(const Dev& D, X& x, uint32_t me, NC& d, uint32_t lo, uint32_t hi) {
+DI void pend_note(const Dev& D, X& x, uint32_t me, NC& d, uint32_t lo, uint32_t hi,
+                  uint32_t olo_early = 0, uint32_t ohi_early = 0) {
   uint32_t plo = lo, phi = hi;
   if (x.now <= d.pexp) {
+#if MR_PLO_EARLY  // loaded with the node record (unchanged in the event while x.now <= pexp)
+    uint32_t olo = olo_early, ohi = ohi_early;
+#else
     uint32_t olo = ND(NF_PLO, me), ohi = ND(NF_PHI, me);
+#endif
     if (olo <= ohi) { plo = olo < lo ? olo : lo; phi = ohi > hi ? ohi : hi; }
   }
   ND(NF_PLO, me) = plo;
@@ -422,6 +427,12 @@ DI void guard_log_write(const Dev& D, X& x, uint32_t L, uint32_t& pexp, uint32_t
 #define MR_AC 8
 #endif
 constexpr uint32_t AC = MR_AC;  // entries per batch of independent loads in log walks
+#ifndef MR_SEND_EARLY  // a leader's append-term loads issued before the applier (A/B in DESIGN.md §6)
+#define MR_SEND_EARLY 1
+#endif
+#ifndef MR_PLO_EARLY
+#define MR_PLO_EARLY 0
+#endif
 #ifndef MR_AP_PIPE  // software-pipelined applier batches (node_apply); A/B in DESIGN.md §6
 #define MR_AP_PIPE 1
 #endif
@@ -685,6 +696,11 @@ DI void node_event(const Dev& D, X& x, bool is_msg, uint32_t tnode, uint32_t slo
   NC d = load_node(D, x, me);
   PV pv;
   load_peers(D, x, me, pv);
+#if MR_PLO_EARLY
+  const uint2 prange = reinterpret_cast<const uint2*>(NDP(me))[NF_PLO / 2];
+#else
+  const uint2 prange = make_uint2(0u, 0u);
+#endif
   PROF(P_LOAD);
   uint32_t mode = SEND_NONE, peers = 0, rtype = 0, ra = 0, rb = 0, kind;
   const uint32_t others = ((1u << D.n) - 1u) & ~(1u << me);
@@ -880,6 +896,16 @@ DI void node_event(const Dev& D, X& x, bool is_msg, uint32_t tnode, uint32_t slo
     mode = SEND_VOTE; peers = others;
     PROF(P_ELECT);
   }
+#if MR_SEND_EARLY
+  // a leader's appends read our terms at next[p] - 1: issue those loads before the applier's
+  // checker stores (the ring slot is valid whatever the applier does; gated after it)
+  uint32_t rawt[NB];
+#pragma unroll
+  for (uint32_t p = 0; p < NB; p++) {
+    const uint32_t ix = pv.nx[p] - 1u;
+    rawt[p] = (mode == SEND_APPEND && bit(peers, p) && p < D.n && ix != 0u) ? D.log[logi(D, x, me, ix)].term : 0u;
+  }
+#endif
   if (d.applied < d.commit) {  // committed entries reach the tester's applier
     node_apply<S>(D, x, me, d, kvready);
     if (x.code != RUN) return;
@@ -904,7 +930,11 @@ DI void node_event(const Dev& D, X& x, bool is_msg, uint32_t tnode, uint32_t slo
       const uint32_t pv = nxa[p] - 1u;
       const bool ld = bit(peers, p) && nxa[p] > d.snap && pv != 0u && pv != d.snap &&
                       pv != d.last && pv <= lbase;
+#if MR_SEND_EARLY
+      const uint32_t t = ld ? rawt[p] : 0u;
+#else
       const uint32_t t = ld ? D.log[logi(D, x, me, pv)].term : 0u;
+#endif
       LNX(p) = nxa[p];
       LPT(p) = pv == 0u ? 0u : pv == d.snap ? d.snapt : pv == d.last ? d.lastt : pv > lbase ? d.term : t;
     }
@@ -940,7 +970,7 @@ DI void node_event(const Dev& D, X& x, bool is_msg, uint32_t tnode, uint32_t slo
       PROF(P_S_PAY);
     }
   }
-  if (plo_acc <= phi_acc) pend_note(D, x, me, d, plo_acc, phi_acc);
+  if (plo_acc <= phi_acc) pend_note(D, x, me, d, plo_acc, phi_acc, prange.x, prange.y);
   if constexpr (KV) {
     if (kvready) {
       kv_flush(D, x, me, d);
