@@ -431,7 +431,7 @@ constexpr uint32_t AC = MR_AC;  // entries per batch of independent loads in log
 #define MR_SEND_EARLY 1
 #endif
 #ifndef MR_PLO_EARLY
-#define MR_PLO_EARLY 0
+#define MR_PLO_EARLY 1
 #endif
 #ifndef MR_AP_PIPE  // software-pipelined applier batches (node_apply); A/B in DESIGN.md §6
 #define MR_AP_PIPE 1
