@@ -8,8 +8,12 @@ for all of them to a verdict. Inputs (seeds) are generated on the device; all
 state is resident in HBM before the timed region.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--clusters C]
-For N > 1 the driver runs it under torch.distributed.run (one rank per GPU).
-Rank 0 prints ONE JSON line.
+For N > 1 the driver runs it under torch.distributed.run (one rank per GPU); run
+directly with --gpus N > 1 it starts that launcher itself as a child process.
+Rank 0 prints ONE JSON line. Besides the headline workload it times config 3's
+crash-restart + persister variant (`figure_8_unreliable_crash`: tests.rs:612-660's
+crash1/start1 in figure_8_unreliable's loop) on the same shard, reported under
+"variants".
 """
 import argparse
 import glob
@@ -32,11 +36,25 @@ METRIC = "seeds/sec & simulated Raft events/sec, 5-node figure8_unreliable, 1-8 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
 
 
-def bytes_per_event(n):
-    """SURVEY.md §8d algorithmic bytes per event: node SoA read + write
-    (2 * (32 + 8N)) + one 32-B message slot written at send and read at
-    delivery (64); + 12 B per log entry shipped (counted separately)."""
-    return 2 * (32 + 8 * n) + 64
+NODE_B = lambda n: 2 * (32 + 8 * n)  # noqa: E731  node state read + written per node event
+TESTER_B = 2 * 72   # tester frame (pc, result, 8 locals, 5 helper words, u64 arg) read + written
+MSG_B = 32          # one message record: written at enqueue, read at delivery
+ENTRY_B = 16        # one log entry (term, command): LE record
+APPLY_B = 48        # applier: log entry + checker entry read, checker entry written
+
+
+def alg_bytes(c, n):
+    """Algorithmic bytes of a run from its counters: what the simulation must
+    move, counted where it moves. Node events read + write the node's state (SURVEY.md §8d:
+    2 * (32 + 8N)); tester events their frame; every message enqueued is written once and
+    every delivered one read once (clogged / lost sends move nothing); AppendEntries
+    payloads are read by the receiver at delivery (entries_shipped) and every log write is
+    16 B; the applier reads the entry and the checker record and writes the record."""
+    enq = c["msgs_sent"] - c["drop_clog"] - c["drop_loss"] - c["drop_overflow"]
+    return ((c["ev_msg"] + c["ev_timer"]) * NODE_B(n) + c["ev_tester"] * TESTER_B
+            + MSG_B * (enq + c["ev_msg"])
+            + ENTRY_B * (c["entries_shipped"] + c["log_writes"] + 2 * c["entries_materialized"])
+            + APPLY_B * c["applies"])
 
 
 def cpu_baseline(test, seeds_per_proc, procs, safety=False):
@@ -66,16 +84,53 @@ def cpu_baseline(test, seeds_per_proc, procs, safety=False):
 
 def load_pmc(test, clusters):
     """HBM traffic per step-kernel launch from the committed rocprofv3 --pmc
-    summary of the same workload (profiles/pmc_*.json), or None."""
+    summary of the same workload (profiles/pmc_*.json, newest round last), or None."""
     best = None
     for p in sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc_*.json"))):
         try:
             d = json.load(open(p))
         except (OSError, ValueError):
             continue
-        if d.get("test") == test and d.get("clusters") == clusters:
+        if d.get("test") == test and d.get("clusters") == clusters and d.get("abi", 2) >= 3:
             best = d
     return best
+
+
+def relaunch(gpus):
+    """`python bench.py --gpus N` (N > 1) outside torch.distributed.run: start the launcher as
+    a child process (nothing here has touched the GPU) and exit with its code."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", os.environ.get("MASTER_PORT", "29511"),
+           os.path.abspath(__file__)] + sys.argv[1:]
+    sys.exit(subprocess.call(cmd))
+
+
+def time_steps(b, first_seed, total, warmup, steps, barrier):
+    """warmup untimed steps, then `steps` timed ones (barrier + device sync on both sides);
+    every step resets the batch to fresh seeds and runs it to its verdicts."""
+    for j in range(warmup):
+        b.submit(first_seed + j * total)
+        b.finish()
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    acc = []
+    for j in range(steps):
+        b.submit(first_seed + (warmup + j) * total)
+        acc.append(b.finish())  # counters are read inside the timed region (verdict collection)
+    torch.cuda.synchronize()
+    barrier()
+    return time.perf_counter() - t0, acc
+
+
+def summed(acc):
+    keys = ["events", "ev_msg", "ev_timer", "ev_tester", "msgs_sent", "drop_clog", "drop_loss",
+            "drop_overflow", "entries_shipped", "log_writes", "entries_materialized", "applies",
+            "passed", "done"]
+    tot = {k: sum(int(c[k]) for _, c in acc) for k in keys}
+    tot["kernel_ms"] = sum(st["kernel_ms"] for st, _ in acc)
+    tot["launches"] = sum(st["launches"] for st, _ in acc)
+    return tot
 
 
 def main():
@@ -85,17 +140,22 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--clusters", type=int, default=131072, help="clusters (seeds) per GPU")
     ap.add_argument("--test", default="figure_8_unreliable_2c")
+    ap.add_argument("--variant", default="figure_8_unreliable_crash",
+                    help="second workload timed on the same shard ('' = none)")
+    ap.add_argument("--variant-steps", type=int, default=2)
     ap.add_argument("--cpu-seeds", type=int, default=20000, help="cpu_baseline seeds per process")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-safety", action="store_true",
                     help="without the per-event Raft invariant checks (MR_F_SAFETY)")
-    ap.add_argument("--pipeline", action="store_true",
-                    help="two batches, step i+1 queued while step i runs (A/B: 5 %% slower)")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (RCCL) or gloo (one-GPU rehearsal)")
     a = ap.parse_args()
 
-    rank = int(os.environ.get("RANK", 0))
     world = int(os.environ.get("WORLD_SIZE", 1))
+    if "WORLD_SIZE" not in os.environ and a.gpus > 1:
+        relaunch(a.gpus)
+    if world != a.gpus and "WORLD_SIZE" in os.environ and a.gpus != 1:
+        sys.exit(f"--gpus {a.gpus} but WORLD_SIZE={world}")
+    rank = int(os.environ.get("RANK", 0))
     local = int(os.environ.get("LOCAL_RANK", 0)) % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
@@ -112,70 +172,30 @@ def main():
 
     total = a.clusters * world
     base, count = mdist.shard(total, world, rank)
-    mk = lambda: sim.Batch(a.test, count, _abi.README_SEED, cluster_base=base, device=local,
-                           safety=not a.no_safety)
-    # --pipeline: two batches on their own streams, step i+1 queued while step i runs so its
-    # waves take the CUs step i's early-finishing waves free (mr_batch_submit / finish).
-    # Measured 545 K vs 576 K seeds/s without: off by default.
-    bufs = [mk(), mk()] if a.pipeline else [mk()]
-    b = bufs[0]
+    b = sim.Batch(a.test, count, _abi.README_SEED, cluster_base=base, device=local,
+                  safety=not a.no_safety)
     n = int(b.cfg.n_nodes)
-
-    def run_steps(first, k, acc):
-        """steps first..first+k-1, each a fresh batch of seeds, pipelined over `bufs`."""
-        if k <= 0:
-            return
-        bufs[0].submit(_abi.README_SEED + first * total)
-        for j in range(k):
-            if j + 1 < k:
-                bufs[(j + 1) % 2].submit(_abi.README_SEED + (first + j + 1) * total)
-            st, c = bufs[j % 2].finish()
-            acc.append((st, c))
-
-    def run_steps_serial(first, k, acc):
-        for j in range(k):
-            b.submit(_abi.README_SEED + (first + j) * total)
-            acc.append(b.finish())
-
-    go = run_steps if a.pipeline else run_steps_serial
-    go(0, a.warmup, [])
-    barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    acc = []
-    go(a.warmup, a.steps, acc)
-    kernel_ms = 0.0
-    launches = events = shipped = passed = done = 0
-    for st, c in acc:  # counters were read inside the timed region (verdict collection)
-        kernel_ms += st["kernel_ms"]
-        launches += st["launches"]
-        events += c["events"]
-        shipped += c["entries_shipped"]
-        passed += c["passed"]
-        done += c["done"]
-    torch.cuda.synchronize()
-    barrier()
-    elapsed = time.perf_counter() - t0
-    r0_events, r0_shipped = events, shipped
+    elapsed, acc = time_steps(b, _abi.README_SEED, total, a.warmup, a.steps, barrier)
+    b.close()
+    r0 = summed(acc)
     last = acc[-1][1]
+    tot = dict(r0)
     if world > 1:
         elapsed = mdist.allreduce_max(elapsed, device=dev)
-        tot = mdist.allreduce_counters({**last, "events": events, "entries_shipped": shipped,
-                                        "passed": passed, "done": done}, device=dev)
-        events, shipped, passed, done = (tot["events"], tot["entries_shipped"], tot["passed"],
-                                         tot["done"])
+        red = mdist.allreduce_counters({**last, **{k: r0[k] for k in mdist.SUM_KEYS if k in r0}},
+                                       device=dev)
+        tot.update({k: red[k] for k in r0 if k in red})
+        last = red
     seeds = total * a.steps
-    alg_bytes = events * bytes_per_event(n) + 12 * shipped
-    # roofline of the dominant kernel (step_kernel): this rank's algorithmic
-    # bytes over all timed launches / their summed HIP-event durations (events
-    # recorded on the batch's own stream around every launch)
-    r0_bytes = r0_events * bytes_per_event(n) + 12 * r0_shipped
-    kern_s = kernel_ms / 1000.0
+    # roofline of the dominant kernel (step_kernel): this rank's algorithmic bytes over its
+    # timed launches / their summed HIP-event durations (events recorded on the batch's own
+    # stream around every launch; rocprofv3 --kernel-trace agrees, profiles/)
+    r0_bytes = alg_bytes(r0, n)
+    kern_s = r0["kernel_ms"] / 1000.0
     achieved = r0_bytes / kern_s / 1e9 if kern_s > 0 else 0.0
     pmc = load_pmc(a.test, a.clusters)
-    traffic = None
-    if pmc:
-        traffic = pmc.get("hbm_bytes_per_launch")
+    traffic = pmc.get("hbm_bytes_per_launch") if pmc else None
+    per_launch = r0_bytes / max(r0["launches"], 1)
     out = {
         "metric": METRIC,
         "value": round(seeds / elapsed, 1),
@@ -192,28 +212,51 @@ def main():
         "config": {"workload": a.test, "nodes": n, "clusters_per_gpu": a.clusters,
                    "clusters_total": total, "parallelism": f"clusters sharded over {world} GPU(s)",
                    "loss": 0.1, "latency_ms": [1, 27], "safety_checks": not a.no_safety},
-        "events_per_sec": round(events / elapsed, 1),
-        "events_per_seed": round(events / seeds, 1),
-        "pass_rate": round(passed / max(done, 1), 6),
-        "coverage": {"leaders_elected_log2": (tot if world > 1 else last)["cov_leaders"]},
+        "events_per_sec": round(tot["events"] / elapsed, 1),
+        "events_per_seed": round(tot["events"] / seeds, 1),
+        "pass_rate": round(tot["passed"] / max(tot["done"], 1), 6),
+        "drop_overflow": tot["drop_overflow"],
+        "coverage": {"leaders_elected_log2": last["cov_leaders"]},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
                      "traffic": traffic,
+                     "traffic_over_alg": round(traffic / per_launch, 3) if traffic else None,
                      "kernel": "step_kernel",
-                     "launches": launches,
-                     "avg_launch_ms": round(kernel_ms / max(launches, 1), 4),
-                     "alg_bytes_per_launch": round(r0_bytes / max(launches, 1)),
-                     "bytes_per_event": bytes_per_event(n)},
-        "alg_bytes_total": alg_bytes,
+                     "launches": r0["launches"],
+                     "avg_launch_ms": round(r0["kernel_ms"] / max(r0["launches"], 1), 4),
+                     "alg_bytes_per_launch": round(per_launch),
+                     "alg_bytes_per_event": round(r0_bytes / max(r0["events"], 1), 1),
+                     "model": "DESIGN.md §6 (node events 2(32+8N), tester 144, 32 B per message "
+                              "enqueued / delivered, 16 B per entry read at delivery / written, "
+                              "48 B per apply)"},
+        "alg_bytes_total": alg_bytes(tot, n),
     }
-    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+    if a.variant:
+        bv = sim.Batch(a.variant, count, _abi.README_SEED, cluster_base=base, device=local,
+                       safety=not a.no_safety)
+        ev, accv = time_steps(bv, _abi.README_SEED, total, 1, a.variant_steps, barrier)
+        bv.close()
+        sv = summed(accv)
+        if world > 1:
+            ev = mdist.allreduce_max(ev, device=dev)
+            red = mdist.allreduce_counters({**accv[-1][1], **{k: sv[k] for k in mdist.SUM_KEYS
+                                                              if k in sv}}, device=dev)
+            sv.update({k: red[k] for k in sv if k in red})
+        out["variants"] = {a.variant: {
+            "value": round(total * a.variant_steps / ev, 1), "unit": "seeds/s",
+            "steps": a.variant_steps, "ms_per_step": round(ev * 1000 / a.variant_steps, 3),
+            "events_per_sec": round(sv["events"] / ev, 1),
+            "events_per_seed": round(sv["events"] / (total * a.variant_steps), 1),
+            "pass_rate": round(sv["passed"] / max(sv["done"], 1), 6),
+            "note": "config 3 read literally: crash1/start1 + persister (tests.rs:612-660) in "
+                    "figure_8_unreliable's loop"}}
+    if rank == 0 and not a.no_cpu_baseline:
         procs = min(16, os.cpu_count() or 1)
-        out["cpu_baseline"] = cpu_baseline(a.test, a.cpu_seeds, procs, safety=not a.no_safety)
+        test = a.test
+        out["cpu_baseline"] = cpu_baseline(test, a.cpu_seeds, procs, safety=not a.no_safety)
         out["gpu_over_cpu"] = round(out["value"] / out["cpu_baseline"]["value"], 2)
     if rank == 0:
         print(json.dumps(out), flush=True)
-    for x in bufs:
-        x.close()
     if world > 1:
         dist.destroy_process_group()
 

@@ -34,9 +34,9 @@
 extern "C" {
 #endif
 
-#define MR_ABI_VERSION 2u
+#define MR_ABI_VERSION 3u
 #define MR_MAX_NODES 8u
-#define MR_MAX_MSG_SLOTS 64u
+#define MR_MAX_MSG_SLOTS 256u
 #define MR_MAX_AE 32u
 
 /* ---- scenarios: one id per reference #[madsim::test] (src/raft/tests.rs) ---- */
@@ -175,6 +175,9 @@ enum mr_fail {
   MR_FAIL_KV_NO_COMPLETION = 47,     /* kvraft/tests.rs:333-337 */
   MR_FAIL_KV_CHECK = 48,             /* kvraft/tester.rs:266-271 Clerk::check */
   MR_FAIL_SAFETY_LOG_MATCHING = 49,  /* MR_F_SAFETY: same index and term, different command */
+  /* the as-shipped service skeleton (MR_F_NULL_RAFT on kvraft / shard_ctrler tests) */
+  MR_FAIL_TODO_APPLY = 50,           /* kvraft/server.rs:69 "not yet implemented: apply command" */
+  MR_FAIL_TODO_RPC_RESULTS = 51,     /* kvraft/client.rs:59 "not yet implemented: handle RPC results" */
   /* simulator limits (not reference panics): a cluster that hits one is reported, never passed */
   MR_FAIL_SIM_CAPACITY = 60,      /* a log / apply / sequence capacity of the config was exceeded */
   MR_FAIL_SIM_EVENT_LIMIT = 61,   /* cfg.max_events processed without a verdict */
@@ -193,7 +196,8 @@ typedef struct mr_cfg {
   uint32_t iters;         /* scenario loop count override (0 = the reference's) */
   uint32_t log_cap;       /* Raft log ring capacity per node, power of two */
   uint32_t apply_cap;     /* apply-checker index capacity per cluster */
-  uint32_t msg_slots;     /* max in-flight messages per cluster (<= 64) */
+  uint32_t msg_slots;     /* max in-flight messages per cluster (<= 64; <= 256 for
+                           * snapshot_recover_many_clients_3b); more in flight = MR_FAIL_SIM_CAPACITY */
   uint32_t ae_max;        /* max entries per AppendEntries (<= 32) */
   uint32_t hb_us;         /* leader heartbeat period */
   uint32_t elect_lo_us;   /* election timeout U[lo, hi) (raft.rs:262: 150..300 ms) */
@@ -213,11 +217,13 @@ typedef struct mr_counters {
   uint64_t msgs_sent;      /* every send: madsim stat().msg_count (tester.rs:147-149) */
   uint64_t drop_clog;      /* endpoint disconnected at send */
   uint64_t drop_loss;      /* Bernoulli(packet_loss_rate) */
-  uint64_t drop_overflow;  /* more than msg_slots in flight */
+  uint64_t drop_overflow;  /* a send found msg_slots in flight: the cluster fails MR_FAIL_SIM_CAPACITY */
   uint64_t drop_deliver;   /* endpoint disconnected / crashed at delivery */
   uint64_t drop_stale;     /* RPC reply to a killed incarnation */
   uint64_t elections, leaders_elected, applies, snapshots, installs;
-  uint64_t entries_shipped;/* log entries carried by AppendEntries */
+  uint64_t entries_shipped;/* AppendEntries entries read by their receiver (counted at delivery,
+                            * past the prevLogIndex/prevLogTerm check; clogged, lost and rejected
+                            * appends carry none: payloads are zero-copy until delivery) */
   uint64_t virt_time_us;   /* sum of per-cluster virtual end time */
   uint64_t max_inflight, max_log, max_index;
   uint64_t first_fail_cluster; /* global cluster id (UINT64_MAX if none) */
@@ -229,6 +235,10 @@ typedef struct mr_counters {
   /* services (kvraft / shard_ctrler; BASELINE config 5 "linearizability-check counters") */
   uint64_t kv_ops;          /* clerk calls completed */
   uint64_t kv_checked;      /* Get results the tester verified against their linearizable value */
+  /* ABI 3 */
+  uint64_t log_writes;      /* log entries written (leader start() appends + follower appends) */
+  uint64_t entries_materialized; /* zero-copy payload entries copied before their log slot was
+                                  * overwritten (HIP path only; the oracle copies at send) */
 } mr_counters;
 
 typedef struct mr_run_stats {

@@ -7,7 +7,7 @@ import ctypes as C
 
 import numpy as np
 
-MR_ABI_VERSION = 2
+MR_ABI_VERSION = 3
 MR_MAX_NODES = 8
 MR_RUNNING = 0xFFFF
 MR_PASS = 0
@@ -66,7 +66,8 @@ FAIL_NAMES = {
     37: "CTRL_MOVE_WRONG", 38: "CTRL_MINIMAL_JOIN", 39: "CTRL_MINIMAL_LEAVE", 40: "CTRL_NO_LEADER",
     41: "CTRL_SAME_CONFIG", 42: "SAFETY_ELECTION", 43: "SAFETY_COMPLETENESS",
     44: "KV_LOG_SIZE", 45: "KV_SNAPSHOT_SIZE", 46: "KV_MINORITY_PROGRESS", 47: "KV_NO_COMPLETION",
-    48: "KV_CHECK", 49: "SAFETY_LOG_MATCHING", 60: "SIM_CAPACITY",
+    48: "KV_CHECK", 49: "SAFETY_LOG_MATCHING", 50: "TODO_APPLY", 51: "TODO_RPC_RESULTS",
+    60: "SIM_CAPACITY",
     61: "SIM_EVENT_LIMIT", 62: "SIM_BAD_PROGRAM", 0xFFFF: "RUNNING",
 }
 
@@ -91,7 +92,8 @@ class MrCounters(C.Structure):
         "virt_time_us", "max_inflight", "max_log", "max_index", "first_fail_cluster",
         "first_fail_code")] + [("fail_hist", C.c_uint64 * 64), ("cov_leaders", C.c_uint64 * 16),
                                ("cov_events", C.c_uint64 * 16), ("kv_ops", C.c_uint64),
-                               ("kv_checked", C.c_uint64)]
+                               ("kv_checked", C.c_uint64), ("log_writes", C.c_uint64),
+                               ("entries_materialized", C.c_uint64)]
 
     def to_dict(self):
         d = {n: getattr(self, n) for n, _ in self._fields_

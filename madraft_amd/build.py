@@ -26,6 +26,9 @@ def _stale(out, srcs):
 # over several translation units of mr_kernel.hip compiled in parallel
 SCN_IDS = list(range(1, 46))
 N_GROUPS = 8
+# scenarios whose kernels carry 256 message slots (snapshot_recover_many_clients_3b: up to
+# 229 messages in flight with 20 clerks)
+WIDE_SLOTS = {42}
 
 
 # the scenarios' default server counts (mr_dev.h k_default_n): each scenario
@@ -40,17 +43,28 @@ def _units(csrc, scns=None):
         ids = [i for i in (scns or SCN_IDS) if nb == 8 or DEFAULT_N[i] == nb]
         if not ids:
             continue
-        ng = max(1, min(N_GROUPS, (len(ids) + 2) // 3))
+        wide = [i for i in ids if i in WIDE_SLOTS]
+        ids = [i for i in ids if i not in WIDE_SLOTS]
+        ng = max(1, min(N_GROUPS, (len(ids) + 2) // 3)) if ids else 0
         for g in range(ng):
             lst = " ".join(f"MR_INST({i})" for i in ids[g::ng])
             units.append((kern, f"nb{nb}_{g}", ["-DMR_COMMON=0", f"-DMR_SCN_LIST={lst}",
                                                 f"-DMR_NB={nb}"]))
+        for i in wide:  # 256 message slots (mr_kernel.hip MR_MW)
+            units.append((kern, f"nb{nb}_w{i}", ["-DMR_COMMON=0", f"-DMR_SCN_LIST=MR_INST({i})",
+                                                 f"-DMR_NB={nb}", "-DMR_MW=4"]))
     ids = list(scns or SCN_IDS)  # decision-tape builds (SEMANTICS §12), NB = 8
-    ng = max(1, min(N_GROUPS, (len(ids) + 3) // 4))
+    wide = [i for i in ids if i in WIDE_SLOTS]
+    ids = [i for i in ids if i not in WIDE_SLOTS]
+    ng = max(1, min(N_GROUPS, (len(ids) + 3) // 4)) if ids else 0
     for g in range(ng):
         lst = " ".join(f"MR_INST({i})" for i in ids[g::ng])
         units.append((kern, f"tape_{g}", ["-DMR_COMMON=0", "-DMR_TAPE=1", f"-DMR_SCN_LIST={lst}",
                                           "-DMR_NB=8"]))
+    for i in wide:
+        units.append((kern, f"tape_w{i}", ["-DMR_COMMON=0", "-DMR_TAPE=1",
+                                           f"-DMR_SCN_LIST=MR_INST({i})", "-DMR_NB=8",
+                                           "-DMR_MW=4"]))
     host = ["-DMR_DEV_SCNS=" + " ".join(f"MR_INST({i})" for i in scns)] if scns else []
     for src in sorted(glob.glob(os.path.join(csrc, "*.cpp"))):
         units.append((src, os.path.splitext(os.path.basename(src))[0], host))

@@ -31,7 +31,8 @@ enum : uint32_t { ST_TESTER = 1, ST_ELECT = 2, ST_NET = 3 };
 enum : uint32_t {
   CNT_EV_MSG, CNT_EV_TIMER, CNT_EV_TESTER, CNT_DROP_CLOG, CNT_DROP_LOSS, CNT_DROP_OVERFLOW,
   CNT_DROP_DELIVER, CNT_DROP_STALE, CNT_ELECTIONS, CNT_LEADERS, CNT_APPLIES, CNT_SNAPSHOTS,
-  CNT_INSTALLS, CNT_SHIPPED, CNT_MAX_INFLIGHT, CNT_MAX_LOG, CNT_MAX_INDEX, CNT__N
+  CNT_INSTALLS, CNT_SHIPPED, CNT_LOG_WRITES, CNT_MATERIALIZED,
+  CNT_MAX_INFLIGHT, CNT_MAX_LOG, CNT_MAX_INDEX, CNT__N
 };
 
 // tester coroutine frame (per cluster): program counter, script locals,
@@ -58,7 +59,9 @@ enum : uint32_t {
   CS__N
 };
 // cs64 [C64__N][C]: per-cluster u64 scalars
-enum : uint32_t { C64_FREE, C64_DIGEST, C64_MMIN, C64_THV, C64_TV, C64__N = C64_TV + T_NV };
+// C64_FREE1..3: free-slot mask words 1..3 (slots 64..255, MR_MW = 4 units)
+enum : uint32_t { C64_FREE, C64_DIGEST, C64_MMIN, C64_THV, C64_TV, C64_FREE1 = C64_TV + T_NV,
+                  C64__N = C64_FREE1 + 3 };
 // nd32 [C][n][NREC]: one 128-B record per node. Words 0..11 are the scalars
 // an event loads / stores as a block (load_node), 12..13 the pending payload
 // range, 14..15 the snapshot value (u64), 16..23 next[p], 24..31 match[p]

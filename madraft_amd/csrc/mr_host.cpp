@@ -156,6 +156,8 @@ const char* mr_fail_message(uint32_t code) {
     case MR_FAIL_KV_NO_COMPLETION: return "put/get did not complete";
     case MR_FAIL_KV_CHECK: return "get(key) check failed";
     case MR_FAIL_SAFETY_LOG_MATCHING: return "log matching: same index and term, different entries";
+    case MR_FAIL_TODO_APPLY: return "not yet implemented: apply command";
+    case MR_FAIL_TODO_RPC_RESULTS: return "not yet implemented: handle RPC results";
     case MR_FAIL_SIM_CAPACITY: return "simulator capacity exceeded";
     case MR_FAIL_SIM_EVENT_LIMIT: return "simulator event limit exceeded";
     case MR_FAIL_SIM_BAD_PROGRAM: return "scenario program error";
@@ -183,7 +185,9 @@ int mr_cfg_init(mr_cfg* c, uint32_t scn) {
                : churn ? 4096 : scn == MR_SCN_UNRELIABLE_AGREE_2C ? 1024 : 0;
   c->log_cap = cap ? cap : 256;
   c->apply_cap = cap ? cap : (snap ? 1024 : 512);
-  c->msg_slots = kv ? 64 : 32;
+  /* in-flight maxima over 64K / 1K seeds: 20 (figure_8), <= 45 (7 / 8 servers,
+   * kvraft), 229 (20 clerks); a send past msg_slots fails the cluster (MR_FAIL_SIM_CAPACITY) */
+  c->msg_slots = scn == MR_SCN_KV_SNAPSHOT_RECOVER_MANY_CLIENTS_3B ? 256 : kv ? 64 : 32;
   c->ae_max = 16;
   c->hb_us = 50000;
   c->elect_lo_us = 150000;  // raft.rs:262
@@ -201,7 +205,9 @@ static int validate(const mr_cfg* c) {
   if (c->n_clusters == 0 || c->n_clusters > (1ull << 31)) return set_err("bad n_clusters");
   if (c->log_cap < 16 || (c->log_cap & (c->log_cap - 1))) return set_err("log_cap: power of 2 >= 16");
   if (c->apply_cap < 16) return set_err("apply_cap too small");
-  if (c->msg_slots < 1 || c->msg_slots > MR_MAX_MSG_SLOTS) return set_err("msg_slots must be 1..64");
+  if (c->msg_slots < 1 || c->msg_slots > MR_MAX_MSG_SLOTS ||
+      (c->msg_slots > 64 && c->scenario != MR_SCN_KV_SNAPSHOT_RECOVER_MANY_CLIENTS_3B))
+    return set_err("msg_slots must be 1..64 (1..256 for snapshot_recover_many_clients_3b)");
   if (c->ae_max < 1 || c->ae_max > MR_MAX_AE) return set_err("ae_max must be 1..32");
   if (c->elect_hi_us <= c->elect_lo_us || c->hb_us == 0) return set_err("bad timers");
   if (c->max_events == 0) return set_err("max_events must be > 0");
@@ -489,6 +495,8 @@ int mr_batch_counters(mr_batch* b, mr_counters* out) {
   }
   out->kv_ops = h[CNT__N + 104];
   out->kv_checked = h[CNT__N + 105];
+  out->log_writes = h[CNT_LOG_WRITES];
+  out->entries_materialized = h[CNT_MATERIALIZED];
   out->first_fail_code = 0;
   if (out->first_fail_cluster != ~0ull) {
     uint32_t code = 0;

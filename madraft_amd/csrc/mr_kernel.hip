@@ -42,6 +42,13 @@ namespace mr {
 #define MR_NB MR_MAX_NODES
 #endif
 constexpr uint32_t NB = MR_NB;
+// message-slot bound of this translation unit: MR_MW 64-bit words of the free-slot mask
+// (1: up to 64 slots; the 20-client snapshot_recover_many_clients_3b keeps up to 229
+// messages in flight, so its unit is built with MR_MW = 4: 256 slots)
+#ifndef MR_MW
+#define MR_MW 1
+#endif
+constexpr uint32_t MW = MR_MW;
 constexpr uint32_t INF_T = 0xFFFFFFFFu;
 constexpr uint32_t LOSS_Q32 = 429496729u;  // floor(0.1 * 2^32), tester.rs:130
 [[maybe_unused]] constexpr uint64_t FNV_OFF = 0xCBF29CE484222325ull;
@@ -56,7 +63,7 @@ struct X {
   uint32_t sleep_us, yield, twake;  // twake: the tester's next wake-up (CS_TWAKE)
   uint32_t cwake, ctid, cslot;      // kvraft: earliest client thread (wake, tid, slot)
   uint32_t conn, alive;  // node bit masks: connected (net clog state), started (tester.rs:24-25)
-  uint64_t free_mask, digest, mmin;
+  uint64_t free_mask[MW], digest, mmin;
   uint32_t timer[NB];  // node timers (election / heartbeat deadline), INF_T = none
 #if !MR_CNT_MEM
   uint32_t cnt[CNT__N];
@@ -78,7 +85,8 @@ struct X {
 // message keys of the lane's cluster live in LDS during a launch: [slot][lane],
 // so a wave's 64 lanes read 64 consecutive u64 (conflict-free). Free slots hold
 // ~0, so the earliest-message scan is a branch-free min over all M slots.
-constexpr uint32_t STEP_BLOCK = 128;
+// lanes per block: 128, or 64 where 256 slots of keys must fit the 160 KiB of LDS
+constexpr uint32_t STEP_BLOCK = MW > 2 ? 64 : 128;
 extern __shared__ uint64_t s_keys[];
 #define LK(s) s_keys[(s) * STEP_BLOCK + threadIdx.x]
 // send-loop staging after the M keys: next[p] and term at next[p] - 1 (u32)
@@ -347,11 +355,28 @@ DI int net_send(const Dev& D, X& x, uint32_t src, uint32_t& nctr, uint32_t dst, 
   }
   philox(D, x, ctr, src, ST_NET, w0, w1);
   if (w0 < net_loss(x)) { CADD(CNT_DROP_LOSS, 1u); return -1; }
-  if (x.inflight >= D.M) { CADD(CNT_DROP_OVERFLOW, 1u); return -1; }
+  if (x.inflight >= D.M) {  // madsim's net has no cap: a full slot table is a simulator limit
+    CADD(CNT_DROP_OVERFLOW, 1u);
+    fail(D, x, MR_FAIL_SIM_CAPACITY);
+    return -1;
+  }
   if (seq >= (1u << 25)) { fail(D, x, MR_FAIL_SIM_CAPACITY); return -1; }  // SEMANTICS §3, §9
   uint32_t t = x.now + u_range(w1, 1000u, net_lat_hi(x));
-  uint32_t slot = (uint32_t)__builtin_ctzll(x.free_mask);
-  x.free_mask &= ~(1ull << slot);
+  uint32_t slot = 0;
+  if constexpr (MW == 1) {
+    slot = (uint32_t)__builtin_ctzll(x.free_mask[0]);
+    x.free_mask[0] &= ~(1ull << slot);
+  } else {
+    bool got = false;
+#pragma unroll
+    for (uint32_t w = 0; w < MW; w++) {
+      if (!got && x.free_mask[w]) {
+        slot = 64u * w + (uint32_t)__builtin_ctzll(x.free_mask[w]);
+        x.free_mask[w] &= x.free_mask[w] - 1ull;
+        got = true;
+      }
+    }
+  }
   // key = (time, seq, dst): ordered as (time, seq) since seq is unique; dst (5
   // bits) in the low bits lets a delivery load the node's state before the message body
   uint64_t key = ((uint64_t)t << 32) | (seq << 5) | dst;
@@ -394,11 +419,17 @@ DI void pend_note(const Dev& D, X& x, uint32_t me, NC& d, uint32_t lo, uint32_t 
   d.pexp = x.now + LAT_BOUND_US;
 }
 
-// copy the payload of every unmaterialized AppendEntries from node L still in flight
-DI void materialize(const Dev& D, X& x, uint32_t L) {
-  uint64_t occ = ~x.free_mask & (D.M >= 64 ? ~0ull : ((1ull << D.M) - 1ull));
+// copy the payload of every unmaterialized AppendEntries from node L still in flight; L's
+// pending range becomes empty and its deadline pexp 0, so no copy of the old range (a
+// node event's early PLO/PHI load, MR_PLO_EARLY) is used again: pend_note merges the old
+// range only while x.now <= pexp
+DI void materialize(const Dev& D, X& x, uint32_t L, uint32_t& pexp) {
+#pragma unroll
+  for (uint32_t w = 0; w < MW; w++) {
+  const uint32_t mw = D.M > 64u * w ? D.M - 64u * w : 0u;  // slots of word w
+  uint64_t occ = ~x.free_mask[w] & (mw >= 64 ? ~0ull : ((1ull << mw) - 1ull));
   while (occ) {
-    const uint32_t s = (uint32_t)__builtin_ctzll(occ);
+    const uint32_t s = 64u * w + (uint32_t)__builtin_ctzll(occ);
     occ &= occ - 1ull;
     const uint32_t hdr = MS32(MF_HDR, s), k = hdr_k(hdr);
     if (hdr_type(hdr) != M_AE_REQ || hdr_src(hdr) != L || (hdr & HDR_MAT) || k == 0) continue;
@@ -406,9 +437,12 @@ DI void materialize(const Dev& D, X& x, uint32_t L) {
     LE* pp = D.pay + ((size_t)x.c * D.M + s) * D.K;
     for (uint32_t j = 0; j < k; j++) pp[j] = D.log[logi(D, x, L, prev + 1 + j)];
     MS32(MF_HDR, s) = hdr | HDR_MAT;
+    CADD(CNT_MATERIALIZED, k);
+  }
   }
   ND(NF_PLO, L) = 1u;  // empty range
   ND(NF_PHI, L) = 0u;
+  pexp = 0;
 }
 
 // before node L (pending deadline pexp) overwrites log index i
@@ -418,8 +452,7 @@ DI void guard_log_write(const Dev& D, X& x, uint32_t L, uint32_t& pexp, uint32_t
   if (plo > phi) return;
   const uint32_t span = phi - plo;  // referenced j in [plo, phi] shares i's slot iff j = i mod cap
   if (span < D.log_cap - 1u && ((i - plo) & (D.log_cap - 1u)) > span) return;
-  materialize(D, x, L);
-  pexp = 0;
+  materialize(D, x, L, pexp);
 }
 
 // ---------------------------------------------------------------- tester storage
@@ -681,7 +714,12 @@ DI void node_event(const Dev& D, X& x, bool is_msg, uint32_t tnode, uint32_t slo
     k = hdr_k(hdr);
     hdr_bits = hdr;
     LK(slot) = ~0ull;
-    x.free_mask |= 1ull << slot;
+    if constexpr (MW == 1) {
+      x.free_mask[0] |= 1ull << slot;
+    } else {
+#pragma unroll
+      for (uint32_t w = 0; w < MW; w++) x.free_mask[w] |= (slot >> 6) == w ? 1ull << (slot & 63u) : 0ull;
+    }
     x.inflight--;
     rescan_min(D, x);
     PROF(P_DECODE);
@@ -803,6 +841,7 @@ DI void node_event(const Dev& D, X& x, bool is_msg, uint32_t tnode, uint32_t slo
           rb = xx;
           break;
         }
+        CADD(CNT_SHIPPED, k - j0);  // the payload entries this receiver reads (zero-copy until here)
         for (uint32_t j = j0; j < k; j += AC) {
           if (j != j0) ae_load_batch(D, x, me, d, src, mat, pp, ma, k, j, pe, lt);
           if (D.safety) {  // MR_F_SAFETY log matching: same index and term => same entry
@@ -827,6 +866,7 @@ DI void node_event(const Dev& D, X& x, bool is_msg, uint32_t tnode, uint32_t slo
             if (i - d.snap > D.log_cap) { fail(D, x, MR_FAIL_SIM_CAPACITY); return; }
             guard_log_write(D, x, me, d.pexp, i);
             D.log[logi(D, x, me, i)] = pe[q];
+            CADD(CNT_LOG_WRITES, 1u);
             d.last = i;
             d.lastt = pe[q].term;
             CMAX(CNT_MAX_LOG, i - d.snap);
@@ -957,7 +997,6 @@ DI void node_event(const Dev& D, X& x, bool is_msg, uint32_t tnode, uint32_t slo
         sk = d.last - prev;
         if (sk > D.K) sk = D.K;
         st = M_AE_REQ; sa = prev; sb = LPT(p); sc = d.commit;
-        CADD(CNT_SHIPPED, sk);
       }
     }
     PROF(P_S_SETUP);
@@ -1037,6 +1076,7 @@ DI bool t_start(const Dev& D, X& x, uint32_t i, uint64_t v, uint32_t& idx, uint3
   guard_log_write(D, x, i, pexp, last);
   ND(NF_PEXP, i) = pexp;
   D.log[li] = LE{term, 0u, v};
+  CADD(CNT_LOG_WRITES, 1u);
   ND(NF_LAST, i) = last;
   ND(NF_LASTT, i) = term;
   CMAX(CNT_MAX_LOG, last - snap);
@@ -1176,7 +1216,9 @@ __global__ void __launch_bounds__(STEP_BLOCK, MR_WAVES_PER_EU) step_kernel(Dev D
     if constexpr (nthr(S) > 0) { x.cwake = CS(CS_CWAKE); x.ctid = CS(CS_CTID); x.cslot = CS(CS_CSLOT); }
 #pragma unroll
     for (uint32_t d = 0; d < NB; d++) x.timer[d] = d < D.n ? TMR(d) : INF_T;
-    x.free_mask = C64(C64_FREE); x.digest = C64(C64_DIGEST); x.mmin = C64(C64_MMIN);
+#pragma unroll
+    for (uint32_t w = 0; w < MW; w++) x.free_mask[w] = C64(w ? C64_FREE1 + w - 1 : C64_FREE);
+    x.digest = C64(C64_DIGEST); x.mmin = C64(C64_MMIN);
 #if !MR_CNT_MEM
 #pragma unroll
     for (uint32_t k = 0; k < CNT__N; k++) x.cnt[k] = CS(CS_CNT + k);
@@ -1270,7 +1312,9 @@ __global__ void __launch_bounds__(STEP_BLOCK, MR_WAVES_PER_EU) step_kernel(Dev D
 #pragma unroll
   for (uint32_t d = 0; d < NB; d++)
     if (d < D.n) TMR(d) = x.timer[d];
-  C64(C64_FREE) = x.free_mask; C64(C64_DIGEST) = x.digest; C64(C64_MMIN) = x.mmin;
+#pragma unroll
+  for (uint32_t w = 0; w < MW; w++) C64(w ? C64_FREE1 + w - 1 : C64_FREE) = x.free_mask[w];
+  C64(C64_DIGEST) = x.digest; C64(C64_MMIN) = x.mmin;
 #if !MR_CNT_MEM
 #pragma unroll
   for (uint32_t k = 0; k < CNT__N; k++) CS(CS_CNT + k) = x.cnt[k];
@@ -1291,7 +1335,10 @@ __global__ void __launch_bounds__(256) reset_kernel(Dev D) {
   for (uint32_t f = 0; f < CS__N; f++) CS(f) = 0;
   CS(CS_CODE) = RUN;
   for (uint32_t f = 0; f < C64__N; f++) C64(f) = 0;
-  C64(C64_FREE) = D.M >= 64 ? ~0ull : ((1ull << D.M) - 1ull);
+  for (uint32_t w = 0; w < 4; w++) {  // the first M slots are free
+    const uint32_t mw = D.M > 64u * w ? D.M - 64u * w : 0u;
+    C64(w ? C64_FREE1 + w - 1 : C64_FREE) = mw >= 64 ? ~0ull : ((1ull << mw) - 1ull);
+  }
   C64(C64_DIGEST) = FNV_OFF;
   C64(C64_MMIN) = ~0ull;
   for (uint32_t d = 0; d < D.n; d++) {

@@ -17,7 +17,8 @@ from ._abi import FAIL_NAMES
 SUM_KEYS = ["clusters", "done", "passed", "failed", "events", "ev_msg", "ev_timer", "ev_tester",
             "msgs_sent", "drop_clog", "drop_loss", "drop_overflow", "drop_deliver", "drop_stale",
             "elections", "leaders_elected", "applies", "snapshots", "installs",
-            "entries_shipped", "virt_time_us", "kv_ops", "kv_checked"]
+            "entries_shipped", "virt_time_us", "kv_ops", "kv_checked", "log_writes",
+            "entries_materialized"]
 MAX_KEYS = ["max_inflight", "max_log", "max_index"]
 COV_KEYS = ["cov_leaders", "cov_events"]
 NO_FAIL = (1 << 63) - 1
@@ -35,8 +36,11 @@ def allreduce_counters(c, device=None, group=None):
     dev = device if device is not None else torch.device("cpu")
     s = torch.tensor([int(c[k]) for k in SUM_KEYS], dtype=torch.int64, device=dev)
     m = torch.tensor([int(c[k]) for k in MAX_KEYS], dtype=torch.int64, device=dev)
-    ff = int(c.get("first_fail_cluster", NO_FAIL))
-    ff = NO_FAIL if ff >= NO_FAIL else ff
+    # the first failing global cluster and ITS code, reduced as one key (cluster << 16 | code)
+    # so the pair always comes from the same rank
+    ff = c.get("first_fail_cluster", None)
+    ff = NO_FAIL if ff is None or int(ff) >= (NO_FAIL >> 16) else \
+        (int(ff) << 16) | (int(c.get("first_fail_code", 0)) & 0xFFFF)
     f = torch.tensor([ff], dtype=torch.int64, device=dev)
     names = sorted(FAIL_NAMES.items())
     code_of = {v: k for k, v in names}
@@ -57,7 +61,9 @@ def allreduce_counters(c, device=None, group=None):
         out[k] = [int(v) for v in sl[base + 16 * j: base + 16 * (j + 1)]]
     out.update({k: int(v) for k, v in zip(SUM_KEYS, sl)})
     out.update({k: int(v) for k, v in zip(MAX_KEYS, m.tolist())})
-    out["first_fail_cluster"] = None if int(f.item()) == NO_FAIL else int(f.item())
+    fv = int(f.item())
+    out["first_fail_cluster"] = None if fv == NO_FAIL else fv >> 16
+    out["first_fail_code"] = 0 if fv == NO_FAIL else fv & 0xFFFF
     return out
 
 

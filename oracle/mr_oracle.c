@@ -291,7 +291,8 @@ static void net_send(OSim* s, uint32_t src, uint32_t dst, OMsg* m) {
   draw(s, ctr, w);
   if (!host_conn(s, src) || !host_conn(s, dst) || !link_up(s, src, dst)) { s->r.drop_clog++; return; }
   if (w[0] < s->loss) { s->r.drop_loss++; return; }
-  if (s->inflight >= s->cfg.msg_slots) { s->r.drop_overflow++; return; }
+  /* madsim's net has no in-flight cap: a full slot table is a simulator limit, not loss */
+  if (s->inflight >= s->cfg.msg_slots) { s->r.drop_overflow++; t_fail(s, MR_FAIL_SIM_CAPACITY); }
   if (seq >= (1u << 25)) t_fail(s, MR_FAIL_SIM_CAPACITY); /* SEMANTICS §3, §9 */
   m->time = s->now + u_range(w[1], s->lat_lo, s->lat_hi);
   m->seq = seq; m->src = (uint8_t)src; m->dst = (uint8_t)dst;
@@ -346,6 +347,7 @@ static void log_put(OSim* s, ONode* d, uint32_t i, uint32_t t, uint64_t v) {
   if (i - d->snap_idx > s->cfg.log_cap) t_fail(s, MR_FAIL_SIM_CAPACITY);
   d->lterm[lpos(s, i)] = t;
   d->lval[lpos(s, i)] = v;
+  s->r.log_writes++;
   d->last = i;
   if (i - d->snap_idx > s->r.max_log) s->r.max_log = i - d->snap_idx;
 }
@@ -592,7 +594,6 @@ static void send_append(OSim* s, uint32_t me, uint32_t p) {
       m.et[j] = d->lterm[lpos(s, prev + 1 + j)];
       m.ev[j] = d->lval[lpos(s, prev + 1 + j)];
     }
-    s->r.entries_shipped += k;
   }
   net_send(s, me, p, &m);
 }
@@ -685,7 +686,9 @@ static void clerk_deliver(OSim* s, OMsg* m) {
 static void kv_request(OSim* s, uint32_t me, OMsg* m) {
   ONode* d = &s->nd[me];
   uint32_t clerk = m->inc; /* the request names its clerk; the reply goes to the sending host */
-  if (s->null_raft || d->role != R_L) {
+  /* the as-shipped skeleton: the RPC handler's Server::apply is todo!() (kvraft/server.rs:69) */
+  if (s->null_raft) t_fail(s, MR_FAIL_TODO_APPLY);
+  if (d->role != R_L) {
     kv_send_rep(s, me, m->src, clerk, m->term, KV_WRONG_LEADER, (me + 1) % s->n, 0, 0);
     return;
   }
@@ -760,6 +763,7 @@ static void deliver(OSim* s, OMsg* m) {
         reply(s, me, m, M_AE_REP, 0, x);
         break;
       }
+      s->r.entries_shipped += m->k - j0; /* the payload entries this receiver reads */
       for (uint32_t j = j0; j < m->k; j++) {
         uint32_t i = m->a + 1 + j;
         if (i <= d->last && term_at(s, d, i) == m->et[j]) {
@@ -1463,6 +1467,8 @@ static void clerk_begin(OSim* s, uint32_t slot, uint32_t op, uint32_t key, uint3
 static int clerk_resume(OSim* s, uint32_t slot) {
   OClerk* c = &s->ck[slot];
   c->waiting = 0;
+  /* the as-shipped ClerkCore::call: todo!() once call_timeout returns (kvraft/client.rs:59) */
+  if (s->null_raft) t_fail(s, MR_FAIL_TODO_RPC_RESULTS);
   if (c->got) {
     if (c->rstat == KV_OK) { s->r.kv_ops++; return 1; }
     c->lh = c->rstat == KV_WRONG_LEADER ? c->rhint : (c->lh + 1) % s->n;
@@ -2307,6 +2313,7 @@ static int sim_alloc(OSim* s, const mr_cfg* cfg) {
   if (cfg->n_nodes < 3 || cfg->n_nodes > MR_MAX_NODES) return -1;
   if (cfg->log_cap < 16 || (cfg->log_cap & (cfg->log_cap - 1))) return -1;
   if (cfg->msg_slots < 1 || cfg->msg_slots > MR_MAX_MSG_SLOTS) return -1;
+  if (cfg->msg_slots > 64 && cfg->scenario != MR_SCN_KV_SNAPSHOT_RECOVER_MANY_CLIENTS_3B) return -1;
   if (cfg->ae_max < 1 || cfg->ae_max > MR_MAX_AE) return -1;
   if (cfg->apply_cap < 16) return -1;
   for (uint32_t i = 0; i < cfg->n_nodes; i++) {
@@ -2407,7 +2414,7 @@ static void acc(mro_result* a, const mro_result* b) {
   a->drop_deliver += b->drop_deliver; a->drop_stale += b->drop_stale;
   a->elections += b->elections; a->leaders_elected += b->leaders_elected;
   a->applies += b->applies; a->snapshots += b->snapshots; a->installs += b->installs;
-  a->entries_shipped += b->entries_shipped;
+  a->entries_shipped += b->entries_shipped; a->log_writes += b->log_writes;
   if (b->max_inflight > a->max_inflight) a->max_inflight = b->max_inflight;
   if (b->max_log > a->max_log) a->max_log = b->max_log;
   if (b->max_index > a->max_index) a->max_index = b->max_index;
@@ -2477,7 +2484,7 @@ int mro_cfg_init(mr_cfg* c, uint32_t scn) {
                : churn ? 4096 : scn == MR_SCN_UNRELIABLE_AGREE_2C ? 1024 : 0;
   c->log_cap = cap ? cap : 256;
   c->apply_cap = cap ? cap : (snap ? 1024 : 512);
-  c->msg_slots = kv ? 64 : 32;
+  c->msg_slots = scn == MR_SCN_KV_SNAPSHOT_RECOVER_MANY_CLIENTS_3B ? 256 : kv ? 64 : 32;
   c->ae_max = 16;
   c->hb_us = 50000;
   c->elect_lo_us = 150000;
@@ -2512,6 +2519,8 @@ const char* mro_fail_message(uint32_t code) {
     case MR_FAIL_KV_NO_COMPLETION: return "put/get did not complete";
     case MR_FAIL_KV_CHECK: return "get(key) check failed";
     case MR_FAIL_SAFETY_LOG_MATCHING: return "log matching: same index and term, different entries";
+    case MR_FAIL_TODO_APPLY: return "not yet implemented: apply command";
+    case MR_FAIL_TODO_RPC_RESULTS: return "not yet implemented: handle RPC results";
     case MR_FAIL_SIM_CAPACITY: return "simulator capacity exceeded";
     case MR_FAIL_SIM_EVENT_LIMIT: return "simulator event limit exceeded";
     default: return "scenario assertion failed";

@@ -36,6 +36,7 @@ typedef struct mro_result {
   uint64_t max_inflight, max_log, max_index;
   uint64_t kv_ops;      /* service clerk calls completed (kvraft / shard_ctrler) */
   uint64_t kv_checked;  /* Get results the tester verified against their linearizable value */
+  uint64_t log_writes;  /* log entries written (leader appends + follower appends) */
 } mro_result;
 
 /* Run cluster `cluster` (global id) of cfg; trace (optional) receives up to

@@ -20,7 +20,7 @@ class MroResult(C.Structure):
             "events", "ev_msg", "ev_timer", "ev_tester", "msgs_sent", "drop_clog", "drop_loss",
             "drop_overflow", "drop_deliver", "drop_stale", "elections", "leaders_elected",
             "applies", "snapshots", "installs", "entries_shipped", "max_inflight", "max_log",
-            "max_index", "kv_ops", "kv_checked")]
+            "max_index", "kv_ops", "kv_checked", "log_writes")]
 
     def to_dict(self):
         return {n: int(getattr(self, n)) for n, _ in self._fields_}

@@ -51,6 +51,7 @@ def _counters_of(oracle, cfg, first, count):
     out.update(clusters=count, done=count, passed=int((code == 0).sum()),
                failed=int((code != 0).sum()),
                first_fail_cluster=(first + int(fails[0])) if fails.size else mdist.NO_FAIL,
+               first_fail_code=int(code[fails[0]]) if fails.size else 0,
                fail_hist=hist)
     return out
 
@@ -91,6 +92,34 @@ def test_gloo_sharded_run_equals_single_process(oracle, test, total, kw):
         assert tot[k] == ref[k], k
     ff = ref["first_fail_cluster"]
     assert tot["first_fail_cluster"] == (None if ff == mdist.NO_FAIL else ff)
+    assert tot["first_fail_code"] == ref["first_fail_code"]
     assert sum(tot["fail_hist"].values()) == total
     assert tmax == 2.0  # max over ranks of the per-rank time (bench.py)
 
+
+
+def _pair_worker(rank, world, port, q):
+    """Rank 0 fails first at a higher cluster id with code 6, rank 1 at a lower one with
+    code 1: the reduced pair must be rank 1's (cluster, code), never mixed across ranks."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    c = {k: 0 for k in mdist.SUM_KEYS + mdist.MAX_KEYS}
+    c.update(first_fail_cluster=[10, 3][rank], first_fail_code=[6, 1][rank], fail_hist={})
+    tot = mdist.allreduce_counters(c)
+    if rank == 0:
+        q.put((tot["first_fail_cluster"], tot["first_fail_code"]))
+    dist.destroy_process_group()
+
+
+def test_first_fail_pair_reduced_together():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_pair_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    got = q.get(timeout=120)
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert got == (3, 1)

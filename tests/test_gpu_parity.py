@@ -20,7 +20,7 @@ SUPPORTED = [n for n in _abi.SCENARIOS if n and n not in _abi.GPU_UNSUPPORTED]
 COUNTER_KEYS = ["events", "ev_msg", "ev_timer", "ev_tester", "msgs_sent", "drop_clog",
                 "drop_loss", "drop_overflow", "drop_deliver", "drop_stale", "elections",
                 "leaders_elected", "applies", "snapshots", "installs", "entries_shipped",
-                "max_inflight", "max_log", "max_index", "kv_ops", "kv_checked"]
+                "max_inflight", "max_log", "max_index", "kv_ops", "kv_checked", "log_writes"]
 
 
 def first_diff(a, b):
@@ -66,6 +66,15 @@ def test_null_node_kat(hip, oracle):
     assert (code == 1).all() and cnt["msgs_sent"] == 0
     code, cnt = compare(hip, oracle, "basic_agree_2b", 64, null_raft=True)
     assert (code == 6).all()
+
+
+@pytest.mark.parametrize("test", ["unreliable_3a", "unreliable_one_key_3a", "snapshot_rpc_3b",
+                                  "multi_4a"])
+def test_null_service_kat(hip, oracle, test):
+    """Skeleton-service KAT on the GPU: kvraft/server.rs:69 / kvraft/client.rs:59 panics,
+    same verdicts, times and traces as the oracle."""
+    code, cnt = compare(hip, oracle, test, 128, null_raft=True)
+    assert np.isin(code, [50, 51]).all() and (code == 50).mean() > 0.8 and cnt["kv_ops"] == 0
 
 
 def test_fail_agree_5_unreliable(hip, oracle):
@@ -123,7 +132,7 @@ def test_step_budget_independence(hip):
 @pytest.mark.parametrize("test,clusters,kw", [
     ("fail_agree_2b", 65536, dict(nodes=5, unreliable=True)),     # BASELINE config 2
     ("figure_8_unreliable_2c", 131072, {}),                        # config 3, one GPU's shard
-    ("snapshot_install_unreliable_2d", 65536, dict(nodes=7)),      # config 4 shape
+    ("snapshot_install_unreliable_2d", 262144, dict(nodes=7)),     # config 4: 256K 7-node / GPU
     ("unreliable_3a", 65536, {}),                                  # config 5: kvraft clerks
 ])
 def test_baseline_sizes(hip, oracle, test, clusters, kw):

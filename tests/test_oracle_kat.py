@@ -58,6 +58,25 @@ def test_skeleton_one_fails_after_10s(oracle, test):
     assert r["ev_tester"] == 1 + 200
 
 
+@pytest.mark.parametrize("test", _abi.KV_TESTS + ["basic_4a", "multi_4a"])
+def test_skeleton_service_panics_at_apply(oracle, test):
+    """The as-shipped kvraft / shard_ctrler service: the first clerk request a server's RPC
+    handler receives hits `todo!("apply command")` (kvraft/server.rs:69, shard_ctrler's
+    Server is the same generic Server); a clerk whose call_timeout returns first hits
+    `todo!("handle RPC results")` (kvraft/client.rs:59) after exactly 500 ms."""
+    cfg = oracle.cfg(test, flags=_abi.MR_F_NULL_RAFT)
+    code, t, _, s = oracle.run_batch(cfg, 0, 64)
+    unrel = test in ("unreliable_3a", "unreliable_one_key_3a") or "unreliable" in test
+    lat_hi = 27_000 if unrel else 10_000
+    assert set(np.unique(code).tolist()) <= ({50, 51} if unrel else {50})
+    apply_ = code == 50
+    assert apply_.mean() > 0.8
+    # every clerk's first request leaves at t = 0 and lands after U[1, lat_hi) ms
+    assert (t[apply_] >= 1_000).all() and (t[apply_] < lat_hi).all()
+    assert (t[code == 51] == 500_000).all()
+    assert s["kv_ops"] == 0 and s["applies"] == 0
+
+
 @pytest.mark.parametrize("test", SUPPORTED)
 def test_reference_assertions_hold(oracle, test):
     """Every in-scope reference test passes on 64 seeds: its own assertions
@@ -66,10 +85,9 @@ def test_reference_assertions_hold(oracle, test):
     code, t, dig, s = oracle.run_batch(cfg, 0, 64)
     assert (code == 0).all(), {int(c): int((code == c).sum()) for c in np.unique(code)}
     assert (t <= 120_000_000).all()
-    # 20 clients' retries exceed the 64 in-flight message slots (Capacities):
-    # overflow drops are counted and act as loss there, on both sides alike
-    if test != "snapshot_recover_many_clients_3b":
-        assert s["drop_overflow"] == 0
+    # madsim's net has no in-flight cap: slot tables are sized so no send finds one full
+    # (a full table would fail the cluster with SIM_CAPACITY, never act as loss)
+    assert s["drop_overflow"] == 0
 
 
 def test_count_2b_budgets(oracle):

@@ -45,7 +45,7 @@ if "FETCH_SIZE" in agg:
     per = (rd + wr) / max(disp.get("FETCH_SIZE", nd), 1)
     print(f"HBM bytes (2*FETCH_SIZE + WRITE_SIZE, KiB->B) = {rd + wr:.4g}; per launch {per:.4g}")
     if a.json:
-        json.dump({"test": a.test, "clusters": a.clusters, "kernel": "step_kernel",
+        json.dump({"test": a.test, "clusters": a.clusters, "kernel": "step_kernel", "abi": 3,
                    "dispatches": disp.get("FETCH_SIZE", nd), "hbm_read_bytes": rd,
                    "hbm_write_bytes": wr, "hbm_bytes_per_launch": per,
                    "counters": dict(agg),
