@@ -120,7 +120,10 @@ static inline uint32_t mr_kv_log_cap(uint32_t s) {
 #define MR_F_BUG_VOTE_TWICE 0x10u /* voters ignore votedFor: two leaders per term possible */
 #define MR_F_BUG_VOTE_STALE 0x20u /* voters skip the up-to-date check (Raft §5.4.1) */
 #define MR_F_BUG_NO_PREV_CHECK 0x40u /* followers skip AppendEntries' prevLogTerm check (§5.3) */
-#define MR_F_RECORD 0x80u    /* record every random draw into the batch's tape (mr_tape_get) */
+#define MR_F_RECORD 0x80u    /* record every random decision of each cluster (mr_batch_get_decisions) */
+/* Known-buggy kvraft servers (SEMANTICS §9): the linearizability checker must catch them */
+#define MR_F_BUG_NO_DEDUP 0x100u   /* servers re-apply a retried Put / Append (no per-clerk dedup) */
+#define MR_F_BUG_STALE_READ 0x200u /* a leader answers Get from its local state, not via the log */
 
 /* ---- verdicts: one code per tester panic site ---- */
 enum mr_fail {
@@ -178,6 +181,9 @@ enum mr_fail {
   /* the as-shipped service skeleton (MR_F_NULL_RAFT on kvraft / shard_ctrler tests) */
   MR_FAIL_TODO_APPLY = 50,           /* kvraft/server.rs:69 "not yet implemented: apply command" */
   MR_FAIL_TODO_RPC_RESULTS = 51,     /* kvraft/client.rs:59 "not yet implemented: handle RPC results" */
+  /* the build's linearizability checker (SEMANTICS §9a; the reference's are commented out,
+   * kvraft/tests.rs:386-390,524-528) */
+  MR_FAIL_KV_NOT_LINEARIZABLE = 52,  /* a Get's result fits no linearization of the key's history */
   /* simulator limits (not reference panics): a cluster that hits one is reported, never passed */
   MR_FAIL_SIM_CAPACITY = 60,      /* a log / apply / sequence capacity of the config was exceeded */
   MR_FAIL_SIM_EVENT_LIMIT = 61,   /* cfg.max_events processed without a verdict */
@@ -206,7 +212,7 @@ typedef struct mr_cfg {
   uint32_t trace_clusters;/* with MR_F_TRACE: the first K clusters keep a trace */
   uint32_t trace_cap;     /* trace records per traced cluster */
   int32_t device;         /* HIP device ordinal */
-  uint32_t tape_cap;      /* with MR_F_RECORD: tape words kept per cluster (2 per draw) */
+  uint32_t tape_cap;      /* with MR_F_RECORD: decisions kept per cluster */
   uint32_t reserved[5];
 } mr_cfg;
 
@@ -239,6 +245,7 @@ typedef struct mr_counters {
   uint64_t log_writes;      /* log entries written (leader start() appends + follower appends) */
   uint64_t entries_materialized; /* zero-copy payload entries copied before their log slot was
                                   * overwritten (HIP path only; the oracle copies at send) */
+  uint64_t kv_lin_checked;  /* Get results the linearizability checker verified (SEMANTICS §9a) */
 } mr_counters;
 
 typedef struct mr_run_stats {
@@ -291,21 +298,41 @@ int mr_batch_counters(mr_batch* b, mr_counters* out);
 int mr_trace_get(mr_batch* b, uint32_t k, mr_event* out, size_t cap, size_t* n);
 void mr_batch_destroy(mr_batch* b);
 
-/* ---- decision tapes and replay (docs/SEMANTICS.md §12) ----
- * A tape is a cluster's random draws in the order the simulation makes them, two words
- * (w0, w1) per draw (§2). Replaying a tape makes every draw read it instead of Philox, so a
- * recorder of another simulator's decisions (drops, latencies, timeouts, tester choices,
- * SURVEY.md §8f rank 4) can drive the same run; draws past the end of a tape read (0, 0). */
-/* Drive cluster k of the batch from tape[k * words_per_cluster ..]; 0 words = Philox again.
- * Call after create / reset and before run. */
-int mr_batch_set_tape(mr_batch* b, const uint32_t* tape, uint64_t words_per_cluster);
-/* The words cluster k drew so far (*n, may exceed cap or the tape) and, with MR_F_RECORD or a
- * tape set, up to cap of them. */
-int mr_tape_get(mr_batch* b, uint32_t k, uint32_t* out, size_t cap, size_t* n);
-/* One cluster of cfg (cluster_base selects it) driven by `tape`: its per-event trace (per-node
- * term / role / commit / applied / last / snapshot after every event) and its verdict. */
-int mr_replay(const mr_cfg* cfg, const uint32_t* tape, size_t n_words, mr_event* out, size_t cap,
-              size_t* n_out, uint16_t* code, uint32_t* time_us);
+/* ---- keyed decision traces and replay (docs/SEMANTICS.md §12) ----
+ * Every random choice of a cluster is one decision, keyed by WHO makes it, not by when:
+ *   stream MR_DS_NET    entity = sending host (server i, clerk 8 + k), seq = that host's
+ *                       send index -> w0 < loss_q32 drops the message, w1 picks its latency
+ *                       (madsim net send: drop + latency, tester.rs:127-137);
+ *   stream MR_DS_ELECT  entity = server, seq = its timeout index -> w0 picks the election
+ *                       timeout (raft.rs:260-263, U[150, 300) ms);
+ *   stream MR_DS_TESTER entity = tester thread (0 = the test body), seq = its draw index ->
+ *                       (w0, w1) is the rand::rng() value (tests.rs gen_range / gen_bool /
+ *                       gen_entry as SEMANTICS §2 maps it).
+ * A range choice v in [lo, hi) is the word mr_decision_word(v, lo, hi). A trace is a set:
+ * any order, any subset; a draw whose key is absent takes the seed's own Philox draw and
+ * counts as a miss. A recorder of another simulator's run (a MadSim seed) emits these
+ * records and mr_replay plays them. */
+enum mr_decision_stream { MR_DS_TESTER = 1, MR_DS_ELECT = 2, MR_DS_NET = 3 };
+typedef struct mr_decision {
+  uint32_t cluster; /* batch-relative cluster (mr_replay: ignored) */
+  uint16_t stream;  /* enum mr_decision_stream */
+  uint16_t entity;
+  uint32_t seq;
+  uint32_t w0, w1;
+} mr_decision;
+/* The smallest draw word w with lo + floor(w * (hi - lo) / 2^32) == v (lo <= v < hi). */
+uint32_t mr_decision_word(uint32_t v, uint32_t lo, uint32_t hi);
+/* Drive the batch's clusters by `d` (n records, any order; duplicate keys are an error);
+ * n = 0 = Philox again. Call after create / reset and before run. */
+int mr_batch_set_decisions(mr_batch* b, const mr_decision* d, size_t n);
+/* Cluster k: with MR_F_RECORD its decisions so far in draw order (*n = decisions drawn, up to
+ * cap copied); with decisions set, *n = its draws that found no record (misses). */
+int mr_batch_get_decisions(mr_batch* b, uint32_t k, mr_decision* out, size_t cap, size_t* n);
+/* One cluster of cfg (cluster_base selects the seed for misses) driven by the n decisions:
+ * its per-event trace (per-node term / role / commit / applied / last / snapshot after every
+ * event), its verdict and verdict time, and (misses != NULL) its draws not in `d`. */
+int mr_replay(const mr_cfg* cfg, const mr_decision* d, size_t n, mr_event* out, size_t cap,
+              size_t* n_out, uint16_t* code, uint32_t* time_us, uint64_t* misses);
 
 #ifdef __cplusplus
 }

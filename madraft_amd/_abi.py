@@ -20,6 +20,8 @@ MR_F_BUG_VOTE_TWICE = 0x10
 MR_F_BUG_VOTE_STALE = 0x20
 MR_F_BUG_NO_PREV_CHECK = 0x40
 MR_F_RECORD = 0x80
+MR_F_BUG_NO_DEDUP = 0x100
+MR_F_BUG_STALE_READ = 0x200
 
 README_SEED = 1629626496  # /root/reference/README.md:48
 
@@ -67,6 +69,7 @@ FAIL_NAMES = {
     41: "CTRL_SAME_CONFIG", 42: "SAFETY_ELECTION", 43: "SAFETY_COMPLETENESS",
     44: "KV_LOG_SIZE", 45: "KV_SNAPSHOT_SIZE", 46: "KV_MINORITY_PROGRESS", 47: "KV_NO_COMPLETION",
     48: "KV_CHECK", 49: "SAFETY_LOG_MATCHING", 50: "TODO_APPLY", 51: "TODO_RPC_RESULTS",
+    52: "KV_NOT_LINEARIZABLE",
     60: "SIM_CAPACITY",
     61: "SIM_EVENT_LIMIT", 62: "SIM_BAD_PROGRAM", 0xFFFF: "RUNNING",
 }
@@ -93,7 +96,8 @@ class MrCounters(C.Structure):
         "first_fail_code")] + [("fail_hist", C.c_uint64 * 64), ("cov_leaders", C.c_uint64 * 16),
                                ("cov_events", C.c_uint64 * 16), ("kv_ops", C.c_uint64),
                                ("kv_checked", C.c_uint64), ("log_writes", C.c_uint64),
-                               ("entries_materialized", C.c_uint64)]
+                               ("entries_materialized", C.c_uint64),
+                               ("kv_lin_checked", C.c_uint64)]
 
     def to_dict(self):
         d = {n: getattr(self, n) for n, _ in self._fields_
@@ -122,10 +126,29 @@ EVENT_DTYPE = np.dtype([
 ])
 assert EVENT_DTYPE.itemsize == 32
 
+# keyed decisions (mr_decision, docs/SEMANTICS.md §12)
+MR_DS_TESTER, MR_DS_ELECT, MR_DS_NET = 1, 2, 3
+DECISION_DTYPE = np.dtype([("cluster", "<u4"), ("stream", "<u2"), ("entity", "<u2"), ("seq", "<u4"),
+                           ("w0", "<u4"), ("w1", "<u4")])
+assert DECISION_DTYPE.itemsize == 20
+LOSS_Q32 = 429496729  # floor(0.1 * 2^32), tester.rs:130
+
+
+def decision_word(v, lo, hi):
+    """The smallest draw word w with lo + floor(w * (hi - lo) / 2^32) == v (mr_decision_word)."""
+    assert lo <= v < hi
+    return ((v - lo) << 32) // (hi - lo) + (1 if ((v - lo) << 32) % (hi - lo) else 0)
+
+
+def net_decision(dropped, latency_us=1000, unreliable=True):
+    """(w0, w1) of a send: dropped (by loss) or delivered after latency_us (tester.rs:127-137)."""
+    hi = 27000 if unreliable else 10000
+    return (0 if dropped else 0xFFFFFFFF), decision_word(latency_us, 1000, hi)
+
 # symbols the product library exports (include/madraft_sim.h)
 EXPORTS = [
     "mr_last_error", "mr_fail_message", "mr_scenario_name", "mr_scenario_from_name",
     "mr_cfg_init", "mr_batch_create", "mr_batch_reset", "mr_batch_run", "mr_batch_verdicts",
-    "mr_batch_counters", "mr_trace_get", "mr_batch_destroy", "mr_batch_set_tape", "mr_tape_get",
-    "mr_replay", "mr_batch_submit", "mr_batch_finish",
+    "mr_batch_counters", "mr_trace_get", "mr_batch_destroy", "mr_batch_set_decisions",
+    "mr_batch_get_decisions", "mr_decision_word", "mr_replay", "mr_batch_submit", "mr_batch_finish",
 ]

@@ -48,14 +48,13 @@ enum : uint32_t {
   CS_KVDONE = CS_CNT + CNT__N, CS_MJOIN, CS_CWAKE, CS_CTID, CS_CSLOT,  // tester threads (SEMANTICS §8-9)
   CS_NLIVE,  // live spawned threads
   CS_NOPS,   // shard_ctrler: clerk operations so far
-  CS_LRING,  // MR_F_SAFETY: (term << 4) | leader + 1 by term mod 32
-  CS_LRING_END = CS_LRING + 32,
   CS_CUT,    // server links cut (disconnect2): bit 8 (i mod 4) + j of word CS_CUT + i / 4
   CS_CUT_END = CS_CUT + 2,
   CS_CCUT,   // clerk links cut: bit 8 (k mod 4) + j of word CS_CCUT + k / 4 = clerk host 8 + k !~ server j
   CS_CCUT_END = CS_CCUT + 6,
-  CS_TAPE,   // decision tape: words drawn so far (SEMANTICS §12)
+  CS_TAPE,   // keyed decisions: recorded so far (record) / draws without a record (replay)
   CS_KV_OPS, CS_KV_CHECKED,  // service clerk calls completed / Get results verified
+  CS_KV_LIN,                 // Get results the linearizability checker verified
   CS__N
 };
 // cs64 [C64__N][C]: per-cluster u64 scalars
@@ -103,6 +102,7 @@ enum : uint32_t {
   KT_HL0, KT_HL1,    // generic_test client: hash of its predicted value `last`
   KT_OWN,            // the thread the clerk's calls wake (0 = the test body)
   KT_MCL,            // 1 = a clerk of the test body in a slot that is not a thread
+  KT_LLO,            // a Get's linearizability lower bound at its call (SEMANTICS §9a)
   KT_TOP, KT_TKEY, KT_TELEM, KT_TCNT,  // a task's call: op, key, elem (or appender), calls
   KT__N
 };
@@ -126,6 +126,9 @@ constexpr uint64_t KV_HP = 0x100000001B3ull;  // value hash multiplier
 // index i (slot i / 16 mod 16) holds i at word 0 and the snapshot from word 4
 constexpr uint32_t KVS_W = MAX_CLERKS + KV_KEYS * KV_KW, KV_RING = 16, KRW = 4 + KVS_W;
 constexpr uint32_t KV_SNAP_EVERY = 16;
+// linearizability bookkeeping per (key, appender): tag (cli + 1), appends called, appends
+// acknowledged, largest count a returned Get observed, an all-appenders Get's lower bound
+constexpr uint32_t LINW = 8;
 // ---- shard_ctrler (SEMANTICS §10): per-server append-only config store and a
 // per-cluster table of clerk operations (the log command names an operation)
 constexpr uint32_t N_SHARDS = 10;  // shard_ctrler/mod.rs:9
@@ -137,10 +140,11 @@ enum : uint32_t { OP_TYPE = 0, OP_A, OP_B, OP_NG, OP_GID, OP_ADDR = 9, OPW = 16 
 enum : uint32_t { CT_QUERY = 0, CT_JOIN = 1, CT_LEAVE = 2, CT_MOVE = 3 };
 
 // one tester apply-checker index (StorageHandle, tester.rs:366-428): the value
-// the first applier stored and the mask of servers whose log holds it
+// the first applier stored, the mask of servers whose log holds it, and the
+// entry's term (for the MR_F_SAFETY leader-completeness check)
 struct alignas(16) SE {
   uint64_t val;
-  uint32_t mask, pad;
+  uint32_t mask, term;
 };
 
 // ---- everything the kernels see (passed by value as a kernel argument)
@@ -162,19 +166,24 @@ struct Dev {
   uint32_t* kv32;   // [C][n][KVREC]        (kvraft only)
   uint32_t* kvs32;  // [C][n][KVS_W]        persisted KV snapshots (maxraftstate)
   uint32_t* kring;  // [C][KV_RING][KRW]    recent KV snapshots by index (maxraftstate)
-  uint32_t* tape;   // [C][tape_words]      decision tape (replay / record), else null
-  uint64_t tape_words;
-  uint32_t tape_mode;  // 0 Philox, 1 replay the tape, 2 Philox and record
+  uint4* dtab;      // [C][dcap] keyed decisions {stream << 16 | entity, seq, w0, w1}, else null
+  uint32_t dcap;       // replay: a power of two, each row sorted by key and padded with ~0
+  uint32_t tape_mode;  // 0 Philox, 1 replay keyed decisions, 2 Philox and record them
   uint64_t* cval;   // [C][3][CHURN_VCAP]   churn clients' committed values (churn only)
   uint32_t* cidx;   // [C][3][CHURN_VCAP]   ... and the index each was seen at
   uint32_t* cfg32;  // [C][n][CFG_CAP][CFGW] shard_ctrler config stores
   uint32_t* op32;   // [C][OP_CAP][OPW]       shard_ctrler operations
   uint32_t nthr;    // thread slots of kt32 (0 = none)
   mr_event* trace;  // [trace_clusters][trace_cap]
+  uint32_t* led;    // [C][LED_W] MR_F_SAFETY: bit t = a leader was elected in term t
+  uint32_t* lin32;  // [C][KV_KEYS][KV_APP][LINW] kvraft linearizability bookkeeping (§9a)
   uint32_t* remaining;  // clusters without verdict after a step launch
   unsigned long long* prof;  // [PROF_SLOTS] wave-cycle profile (MR_PROF builds only)
 };
 constexpr uint32_t PROF_SLOTS = 64;
+// election-safety term bitmap (MR_F_SAFETY): terms 0..LED_TERMS-1; a leader elected in a
+// later term is a simulator limit (MR_FAIL_SIM_CAPACITY); figure_8 peaks at term 177
+constexpr uint32_t LED_W = 64, LED_TERMS = 32 * LED_W;
 
 constexpr bool is_kv(uint32_t s) {
   return (s >= MR_SCN_KV_BASIC_3A && s <= MR_SCN_KV_UNRELIABLE_3A) ||

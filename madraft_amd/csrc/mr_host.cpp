@@ -5,6 +5,7 @@
 // stream.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -73,7 +74,7 @@ const uint8_t k_nodes[MR_SCN_COUNT_] = {0, 3, 3, 7, 5, 3, 5, 3, 3, 5, 3, 3, 5, 3
                                         5, 5, 5, 5, 5, 3, 3, 3, 3, 3, 5, 5, 5, 5, 3, 3,
                                         5, 5, 5, 5, 5, 5, 5, 3, 5, 3, 3, 5, 5, 5, 5, 5};
 
-constexpr size_t RED_N = CNT__N + 8 + 64 + 32 + 2;  // reduce_kernel output slots
+constexpr size_t RED_N = CNT__N + 8 + 64 + 32 + 3;  // reduce_kernel output slots
 }  // namespace
 
 struct mr_batch {
@@ -86,7 +87,7 @@ struct mr_batch {
   hipStream_t stream = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   uint32_t budget = 16384;  // events per cluster per launch (MR_STEP_BUDGET)
-  uint32_t* tape = nullptr;  // decision tape (own allocation: set_tape / MR_F_RECORD)
+  uint4* tape = nullptr;     // keyed decisions (own allocation: set_decisions / MR_F_RECORD)
   bool submitted = false;    // mr_batch_submit enqueued a step not yet finished
   std::chrono::steady_clock::time_point t_submit;
 };
@@ -158,6 +159,7 @@ const char* mr_fail_message(uint32_t code) {
     case MR_FAIL_SAFETY_LOG_MATCHING: return "log matching: same index and term, different entries";
     case MR_FAIL_TODO_APPLY: return "not yet implemented: apply command";
     case MR_FAIL_TODO_RPC_RESULTS: return "not yet implemented: handle RPC results";
+    case MR_FAIL_KV_NOT_LINEARIZABLE: return "history is not linearizable";
     case MR_FAIL_SIM_CAPACITY: return "simulator capacity exceeded";
     case MR_FAIL_SIM_EVENT_LIMIT: return "simulator event limit exceeded";
     case MR_FAIL_SIM_BAD_PROGRAM: return "scenario program error";
@@ -213,8 +215,8 @@ static int validate(const mr_cfg* c) {
   if (c->max_events == 0) return set_err("max_events must be > 0");
   if ((c->flags & MR_F_TRACE) && (c->trace_cap == 0 || c->trace_clusters > c->n_clusters))
     return set_err("bad trace config");
-  if ((c->flags & MR_F_RECORD) && (c->tape_cap < 2 || (c->tape_cap & 1u)))
-    return set_err("MR_F_RECORD needs an even tape_cap >= 2");
+  if ((c->flags & MR_F_RECORD) && c->tape_cap < 1)
+    return set_err("MR_F_RECORD needs tape_cap >= 1 (decisions kept per cluster)");
   return 0;
 }
 
@@ -235,7 +237,8 @@ int mr_batch_create(const mr_cfg* cfg, mr_batch** out) {
   D.null_raft = (cfg->flags & MR_F_NULL_RAFT) ? 1u : 0u;
   D.unrel_flag = (cfg->flags & MR_F_UNRELIABLE) ? 1u : 0u;
   D.safety = (cfg->flags & MR_F_SAFETY) ? 1u : 0u;
-  D.bugs = cfg->flags & (MR_F_BUG_VOTE_TWICE | MR_F_BUG_VOTE_STALE | MR_F_BUG_NO_PREV_CHECK);
+  D.bugs = cfg->flags & (MR_F_BUG_VOTE_TWICE | MR_F_BUG_VOTE_STALE | MR_F_BUG_NO_PREV_CHECK |
+                         MR_F_BUG_NO_DEDUP | MR_F_BUG_STALE_READ);
   D.links = kv_gen(cfg->scenario).part ? 1u : 0u;  // server-link cuts (CS_CUT) can exist
   D.trace_clusters = (cfg->flags & MR_F_TRACE) ? cfg->trace_clusters : 0u;
   D.trace_cap = cfg->trace_cap;
@@ -271,6 +274,7 @@ int mr_batch_create(const mr_cfg* cfg, mr_batch** out) {
   D.nthr = nthr(scn);
   if (D.nthr) add(&D.kt32, (size_t)KT__N * D.nthr * C);
   if (is_svc(scn)) add(&D.kv32, (size_t)KVREC * n * C);
+  if (is_kv(scn)) add(&D.lin32, (size_t)KV_KEYS * KV_APP * LINW * C);
   if (kv_gen(scn).maxraft) {
     add(&D.kvs32, (size_t)KVS_W * n * C);
     add(&D.kring, (size_t)KRW * KV_RING * C);
@@ -283,6 +287,7 @@ int mr_batch_create(const mr_cfg* cfg, mr_batch** out) {
     add(&D.cval, (size_t)3 * CHURN_VCAP * C);
     add(&D.cidx, (size_t)3 * CHURN_VCAP * C);
   }
+  if (D.safety) add(&D.led, (size_t)LED_W * C);
   add(&D.trace, (size_t)D.trace_clusters * D.trace_cap);
   add(&D.remaining, 1);
   add(&D.prof, PROF_SLOTS);
@@ -309,13 +314,13 @@ int mr_batch_create(const mr_cfg* cfg, mr_batch** out) {
     p += (it.bytes + 255) & ~size_t(255);
   }
   if (cfg->flags & MR_F_RECORD) {
-    e = hipMalloc(&b->tape, (size_t)C * cfg->tape_cap * sizeof(uint32_t));
+    e = hipMalloc(&b->tape, (size_t)C * cfg->tape_cap * sizeof(uint4));
     if (e != hipSuccess) {
       mr_batch_destroy(b);
       return set_err(std::string("tape allocation failed: ") + hipGetErrorString(e));
     }
-    b->D.tape = b->tape;
-    b->D.tape_words = cfg->tape_cap;
+    b->D.dtab = b->tape;
+    b->D.dcap = cfg->tape_cap;
     b->D.tape_mode = 2;
   }
   if (hipMemset(b->D.prof, 0, PROF_SLOTS * sizeof(unsigned long long)) != hipSuccess) {
@@ -338,8 +343,13 @@ static int enqueue_reset(mr_batch* b, uint64_t seed_base) {
   b->D.seed0 = seed_base + b->cfg.cluster_base;
   HIPCHK(hipSetDevice(b->cfg.device));
   HIPCHK(hipMemsetAsync(b->D.stor, 0, (size_t)b->D.C * b->D.apply_cap * sizeof(SE), b->stream));
+  if (b->D.led)
+    HIPCHK(hipMemsetAsync(b->D.led, 0, (size_t)b->D.C * LED_W * sizeof(uint32_t), b->stream));
   if (b->D.kv32)
     HIPCHK(hipMemsetAsync(b->D.kv32, 0, (size_t)b->D.C * b->D.n * KVREC * sizeof(uint32_t), b->stream));
+  if (b->D.lin32)
+    HIPCHK(hipMemsetAsync(b->D.lin32, 0, (size_t)b->D.C * KV_KEYS * KV_APP * LINW * sizeof(uint32_t),
+                          b->stream));
   if (b->D.kvs32) {
     HIPCHK(hipMemsetAsync(b->D.kvs32, 0, (size_t)b->D.C * b->D.n * KVS_W * sizeof(uint32_t), b->stream));
     HIPCHK(hipMemsetAsync(b->D.kring, 0, (size_t)b->D.C * KV_RING * KRW * sizeof(uint32_t), b->stream));
@@ -495,6 +505,7 @@ int mr_batch_counters(mr_batch* b, mr_counters* out) {
   }
   out->kv_ops = h[CNT__N + 104];
   out->kv_checked = h[CNT__N + 105];
+  out->kv_lin_checked = h[CNT__N + 106];
   out->log_writes = h[CNT_LOG_WRITES];
   out->entries_materialized = h[CNT_MATERIALIZED];
   out->first_fail_code = 0;
@@ -521,25 +532,56 @@ int mr_trace_get(mr_batch* b, uint32_t k, mr_event* out, size_t cap, size_t* n) 
   return 0;
 }
 
-int mr_batch_set_tape(mr_batch* b, const uint32_t* tape, uint64_t words_per_cluster) {
+uint32_t mr_decision_word(uint32_t v, uint32_t lo, uint32_t hi) {
+  if (hi <= lo || v < lo || v >= hi) return 0;
+  // ceil((v - lo) * 2^32 / (hi - lo)): the first w whose range image is v
+  const uint64_t span = hi - lo, num = (uint64_t)(v - lo) << 32;
+  return (uint32_t)((num + span - 1) / span);
+}
+
+int mr_batch_set_decisions(mr_batch* b, const mr_decision* d, size_t n) {
   if (!b) return set_err("null batch");
-  if (words_per_cluster && !tape) return set_err("null tape");
-  if (words_per_cluster & 1u) return set_err("tape words per cluster must be even");
+  if (n && !d) return set_err("null decisions");
   HIPCHK(hipSetDevice(b->cfg.device));
   HIPCHK(hipStreamSynchronize(b->stream));
   if (b->tape) { HIPCHK(hipFree(b->tape)); b->tape = nullptr; }
-  b->D.tape = nullptr; b->D.tape_words = 0; b->D.tape_mode = 0;
-  if (!words_per_cluster) return 0;
-  const size_t bytes = (size_t)b->D.C * words_per_cluster * sizeof(uint32_t);
-  HIPCHK(hipMalloc(&b->tape, bytes));
-  HIPCHK(hipMemcpy(b->tape, tape, bytes, hipMemcpyHostToDevice));
-  b->D.tape = b->tape;
-  b->D.tape_words = words_per_cluster;
+  b->D.dtab = nullptr; b->D.dcap = 0; b->D.tape_mode = 0;
+  if (!n) return 0;
+  const size_t C = b->D.C;
+  std::vector<uint32_t> cnt(C, 0);
+  for (size_t i = 0; i < n; i++) {
+    if (d[i].cluster >= C) return set_err("decision for a cluster outside the batch");
+    if (d[i].stream < MR_DS_TESTER || d[i].stream > MR_DS_NET) return set_err("bad decision stream");
+    cnt[d[i].cluster]++;
+  }
+  uint32_t mx = 1;
+  for (uint32_t c : cnt) mx = c > mx ? c : mx;
+  uint32_t cap = 1;
+  while (cap < mx) cap <<= 1;
+  std::vector<uint4> tab((size_t)C * cap, make_uint4(~0u, ~0u, 0u, 0u));
+  std::vector<uint32_t> fill(C, 0);
+  for (size_t i = 0; i < n; i++) {
+    const mr_decision& r = d[i];
+    tab[(size_t)r.cluster * cap + fill[r.cluster]++] =
+        make_uint4(((uint32_t)r.stream << 16) | r.entity, r.seq, r.w0, r.w1);
+  }
+  auto lt = [](const uint4& a, const uint4& c) { return a.x < c.x || (a.x == c.x && a.y < c.y); };
+  for (size_t c = 0; c < C; c++) {
+    uint4* row = tab.data() + c * cap;
+    std::sort(row, row + cnt[c], lt);
+    for (uint32_t k = 1; k < cnt[c]; k++)
+      if (row[k].x == row[k - 1].x && row[k].y == row[k - 1].y)
+        return set_err("duplicate decision key (cluster " + std::to_string(c) + ")");
+  }
+  HIPCHK(hipMalloc(&b->tape, tab.size() * sizeof(uint4)));
+  HIPCHK(hipMemcpy(b->tape, tab.data(), tab.size() * sizeof(uint4), hipMemcpyHostToDevice));
+  b->D.dtab = b->tape;
+  b->D.dcap = cap;
   b->D.tape_mode = 1;
   return 0;
 }
 
-int mr_tape_get(mr_batch* b, uint32_t k, uint32_t* out, size_t cap, size_t* n) {
+int mr_batch_get_decisions(mr_batch* b, uint32_t k, mr_decision* out, size_t cap, size_t* n) {
   if (!b || !n) return set_err("null argument");
   if (k >= b->D.C) return set_err("cluster out of range");
   HIPCHK(hipSetDevice(b->cfg.device));
@@ -547,18 +589,23 @@ int mr_tape_get(mr_batch* b, uint32_t k, uint32_t* out, size_t cap, size_t* n) {
   uint32_t used = 0;
   HIPCHK(hipMemcpy(&used, b->D.cs32 + (size_t)CS_TAPE * b->D.C + k, 4, hipMemcpyDeviceToHost));
   *n = used;
-  if (!b->tape || !out) return 0;
-  size_t m = used < b->D.tape_words ? used : b->D.tape_words;
+  if (b->D.tape_mode != 2 || !out) return 0;
+  size_t m = used < b->D.dcap ? used : b->D.dcap;
   if (m > cap) m = cap;
-  HIPCHK(hipMemcpy(out, b->tape + (size_t)k * b->D.tape_words, m * sizeof(uint32_t),
-                   hipMemcpyDeviceToHost));
+  std::vector<uint4> rows(m);
+  if (m)
+    HIPCHK(hipMemcpy(rows.data(), b->tape + (size_t)k * b->D.dcap, m * sizeof(uint4),
+                     hipMemcpyDeviceToHost));
+  for (size_t i = 0; i < m; i++)
+    out[i] = mr_decision{k, (uint16_t)(rows[i].x >> 16), (uint16_t)(rows[i].x & 0xFFFFu), rows[i].y,
+                         rows[i].z, rows[i].w};
   return 0;
 }
 
-int mr_replay(const mr_cfg* cfg, const uint32_t* tape, size_t n_words, mr_event* out, size_t cap,
-              size_t* n_out, uint16_t* code, uint32_t* time_us) {
+int mr_replay(const mr_cfg* cfg, const mr_decision* d, size_t n, mr_event* out, size_t cap,
+              size_t* n_out, uint16_t* code, uint32_t* time_us, uint64_t* misses) {
   if (!cfg || !n_out) return set_err("null argument");
-  if (n_words & 1u) return set_err("tape length must be even");
+  if (n && !d) return set_err("null decisions");
   mr_cfg c = *cfg;
   c.n_clusters = 1;
   c.flags = (c.flags | MR_F_TRACE) & ~MR_F_RECORD;
@@ -567,8 +614,12 @@ int mr_replay(const mr_cfg* cfg, const uint32_t* tape, size_t n_words, mr_event*
   mr_batch* b = nullptr;
   int rc = mr_batch_create(&c, &b);
   if (rc) return rc;
-  std::vector<uint32_t> pad(tape ? 0 : 2, 0u);  // an empty tape: every draw reads (0, 0)
-  rc = mr_batch_set_tape(b, tape ? tape : pad.data(), tape ? n_words : 2);
+  std::vector<mr_decision> one(d, d + n);
+  for (auto& r : one) r.cluster = 0;
+  // keyed replay runs the MR_TAPE kernels even for an empty trace (every draw then misses)
+  const mr_decision none{0, MR_DS_TESTER, 0xFFFFu, 0xFFFFFFFFu, 0u, 0u};
+  if (one.empty()) one.push_back(none);
+  rc = mr_batch_set_decisions(b, one.data(), one.size());
   mr_run_stats st;
   if (!rc) rc = mr_batch_run(b, 0, &st);
   uint16_t cd = 0;
@@ -576,6 +627,9 @@ int mr_replay(const mr_cfg* cfg, const uint32_t* tape, size_t n_words, mr_event*
   if (!rc) rc = mr_batch_verdicts(b, &cd, &t, nullptr);
   if (!rc && out && cap) rc = mr_trace_get(b, 0, out, cap, n_out);
   else if (!rc) *n_out = 0;
+  size_t ms = 0;
+  if (!rc && misses) rc = mr_batch_get_decisions(b, 0, nullptr, 0, &ms);
+  if (!rc && misses) *misses = ms;
   if (!rc && code) *code = cd;
   if (!rc && time_us) *time_us = t;
   mr_batch_destroy(b);

@@ -179,26 +179,35 @@ __device__ __forceinline__ uint2 philox2(uint32_t c0, uint32_t c1, uint32_t c2, 
   }
   return make_uint2(c0, c1);
 }
-// the cluster's draw: key = its seed (SEMANTICS §2); in MR_TAPE builds, with a tape set,
-// replay reads the next two words ((0, 0) past the end) and record appends the draw (§12)
+// the cluster's draw: counter (c0, c1, c2) = (seq, entity, stream), key = its seed
+// (SEMANTICS §2). In MR_TAPE builds with keyed decisions set (§12), replay looks the key up
+// in the cluster's sorted table (a miss takes the Philox draw and is counted), and record
+// appends {key, words} in draw order.
 DI void philox(const Dev& D, X& x, uint32_t c0, uint32_t c1, uint32_t c2, uint32_t& w0,
                uint32_t& w1) {
   if constexpr (MR_TAPE) {
     if (D.tape_mode) {
-      const uint32_t p = CS(CS_TAPE);
-      CS(CS_TAPE) = p + 2u;
-      uint32_t* tp = D.tape + (size_t)x.c * D.tape_words;
-      if (D.tape_mode == 1u) {
-        w0 = p < D.tape_words ? tp[p] : 0u;
-        w1 = p + 1u < D.tape_words ? tp[p + 1] : 0u;
+      const uint32_t khi = (c2 << 16) | c1;
+      uint4* tb = D.dtab + (size_t)x.c * D.dcap;
+      if (D.tape_mode == 1u) {  // lower bound over the power-of-two row
+        uint32_t pos = 0;
+        for (uint32_t step = D.dcap >> 1; step; step >>= 1) {
+          const uint4 r = tb[pos + step];
+          if (r.x < khi || (r.x == khi && r.y <= c0)) pos += step;
+        }
+        const uint4 r = tb[pos];
+        if (r.x == khi && r.y == c0) { w0 = r.z; w1 = r.w; return; }
+        CS(CS_TAPE) = CS(CS_TAPE) + 1u;  // no record: the seed's own draw
+      } else {
+        const uint64_t seed = D.seed0 + x.c;
+        const uint2 w = philox2(c0, c1, c2, (uint32_t)seed, (uint32_t)(seed >> 32));
+        w0 = w.x;
+        w1 = w.y;
+        const uint32_t p = CS(CS_TAPE);
+        CS(CS_TAPE) = p + 1u;
+        if (p < D.dcap) tb[p] = make_uint4(khi, c0, w0, w1);
         return;
       }
-      const uint64_t seed = D.seed0 + x.c;
-      const uint2 w = philox2(c0, c1, c2, (uint32_t)seed, (uint32_t)(seed >> 32));
-      w0 = w.x;
-      w1 = w.y;
-      if (p + 1u < D.tape_words) { tp[p] = w0; tp[p + 1] = w1; }
-      return;
     }
   }
   const uint64_t seed = D.seed0 + x.c;
@@ -318,13 +327,26 @@ DI void reset_timer(const Dev& D, X& x, uint32_t d, NC& n) {  // raft.rs:260-263
   set_timer(x, d, x.now + u_range(w0, D.elo, D.ehi));
 }
 
+#ifndef MR_RESCAN_OCC  // scan only the occupied slots (A/B: DESIGN.md §6)
+#define MR_RESCAN_OCC 0
+#endif
 DI void rescan_min(const Dev& D, X& x) {
   uint64_t best = ~0ull;
   uint32_t bs = 0;
+  if constexpr (MR_RESCAN_OCC && MW == 1) {
+    uint64_t occ = ~x.free_mask[0] & (D.M >= 64 ? ~0ull : ((1ull << D.M) - 1ull));
+    while (occ) {
+      const uint32_t s = (uint32_t)__builtin_ctzll(occ);
+      occ &= occ - 1ull;
+      const uint64_t k = LK(s);
+      if (k < best) { best = k; bs = s; }
+    }
+  } else {
 #pragma unroll 8
-  for (uint32_t s = 0; s < D.M; s++) {
-    uint64_t k = LK(s);
-    if (k < best) { best = k; bs = s; }
+    for (uint32_t s = 0; s < D.M; s++) {
+      uint64_t k = LK(s);
+      if (k < best) { best = k; bs = s; }
+    }
   }
   x.mmin = best;
   x.mslot = bs;
@@ -344,16 +366,18 @@ DI bool link_cut(const Dev& D, X& x, uint32_t a, uint32_t b) {
 // :147-149). Returns the slot or -1 if the message is dropped.
 DI int net_send(const Dev& D, X& x, uint32_t src, uint32_t& nctr, uint32_t dst, uint32_t type,
                 uint32_t inc, uint32_t term, uint32_t a, uint32_t b, uint32_t c, uint64_t v,
-                uint32_t k) {
+                uint32_t k, uint32_t ent = NONE) {
+  // the sender in its NET draws: server src, or a clerk's 8 + clerk id (ent; SEMANTICS §12)
+  const uint32_t who = ent == NONE ? src : ent;
   uint32_t seq = x.msgs_sent++;
   uint32_t ctr = nctr++;
   uint32_t w0, w1;
   if (!bit(x.conn, src) || !bit(x.conn, dst) || link_cut(D, x, src, dst)) {
-    if (MR_TAPE && D.tape_mode) philox(D, x, ctr, src, ST_NET, w0, w1);  // its (unused) draw is on the tape
+    if (MR_TAPE && D.tape_mode) philox(D, x, ctr, who, ST_NET, w0, w1);  // recorded too (as the oracle)
     CADD(CNT_DROP_CLOG, 1u);
     return -1;
   }
-  philox(D, x, ctr, src, ST_NET, w0, w1);
+  philox(D, x, ctr, who, ST_NET, w0, w1);
   if (w0 < net_loss(x)) { CADD(CNT_DROP_LOSS, 1u); return -1; }
   if (x.inflight >= D.M) {  // madsim's net has no cap: a full slot table is a simulator limit
     CADD(CNT_DROP_OVERFLOW, 1u);
@@ -552,7 +576,7 @@ DI void node_apply(const Dev& D, X& x, uint32_t me, NC& d, bool& kvready) {
       if (cm[j] && csv[j] != ce[j].val) { fail(D, x, MR_FAIL_APPLY_MISMATCH); return; }  // tester.rs:384
       if (i > len) { fail(D, x, MR_FAIL_APPLY_OUT_OF_ORDER); return; }  // tester.rs:393
       if (i == len) {
-        sb[i] = SE{ce[j].val, cm[j] | (1u << me), 0u};
+        sb[i] = SE{ce[j].val, cm[j] | (1u << me), ce[j].term};
         len++;
         CMAX(CNT_MAX_INDEX, i);
       }
@@ -606,7 +630,7 @@ DI void node_apply(const Dev& D, X& x, uint32_t me, NC& d, bool& kvready) {
       if (m[j] && sv[j] != e[j].val) { fail(D, x, MR_FAIL_APPLY_MISMATCH); return; }  // tester.rs:384
       if (i > len) { fail(D, x, MR_FAIL_APPLY_OUT_OF_ORDER); return; }  // tester.rs:393
       if (i == len) {
-        sb[i] = SE{e[j].val, m[j] | (1u << me), 0u};
+        sb[i] = SE{e[j].val, m[j] | (1u << me), e[j].term};
         len++;
         CMAX(CNT_MAX_INDEX, i);
       }
@@ -654,14 +678,24 @@ DI void advance_commit(const Dev& D, X& x, uint32_t me, NC& d, const uint32_t (&
   if (N > d.commit && N > lbase) d.commit = N;  // term_at(N) == term
 }
 
-// MR_F_SAFETY (SEMANTICS §11): election safety over a ring of the last 32
-// terms' leaders; leader completeness for the highest index any server applied
+// MR_F_SAFETY (SEMANTICS §11) when `me` wins term d.term:
+//  * election safety, exact: one bit per term that has had a leader (a second win in a
+//    term is the violation; a node never wins one term twice, its term only grows);
+//  * leader completeness: the committed entry at the highest index any server applied —
+//    its index, term and command as the apply checker recorded them — is in the new
+//    leader's log (or under its snapshot). By log matching (checked at every
+//    AppendEntries) the same index and term imply every earlier committed entry too.
 DI void safety_on_leader(const Dev& D, X& x, uint32_t me, const NC& d) {
-  const uint32_t t = d.term, e = CS(CS_LRING + (t & 31u));
-  if ((e >> 4) == t && (e & 15u) != me + 1u) { fail(D, x, MR_FAIL_SAFETY_ELECTION); return; }
-  CS(CS_LRING + (t & 31u)) = (t << 4) | (me + 1u);
+  const uint32_t t = d.term;
+  if (t >= LED_TERMS) { fail(D, x, MR_FAIL_SIM_CAPACITY); return; }
+  uint32_t* lw = D.led + (size_t)x.c * LED_W + (t >> 5);
   const uint32_t j = CNT_GET(CNT_MAX_INDEX);
-  if (j > d.snap && (j > d.last || D.log[logi(D, x, me, j)].val != D.stor[(size_t)x.c * D.apply_cap + j].val))
+  const uint32_t w = *lw;
+  const LE le = D.log[logi(D, x, me, j)];
+  const SE se = D.stor[(size_t)x.c * D.apply_cap + j];
+  if ((w >> (t & 31u)) & 1u) { fail(D, x, MR_FAIL_SAFETY_ELECTION); return; }
+  *lw = w | (1u << (t & 31u));
+  if (j > d.snap && (j > d.last || le.val != se.val || le.term != se.term))
     fail(D, x, MR_FAIL_SAFETY_COMPLETENESS);
 }
 
@@ -936,6 +970,14 @@ DI void node_event(const Dev& D, X& x, bool is_msg, uint32_t tnode, uint32_t slo
     mode = SEND_VOTE; peers = others;
     PROF(P_ELECT);
   }
+  // peers a send can reach: one from a disconnected sender or to a disconnected destination
+  // clogs (net_send, SEMANTICS §4), so it needs only its accounting — a sequence number, a
+  // send index, drop_clog — and none of the send path's loads (MR_TAPE builds record its
+  // draw, so they send it the long way)
+#ifndef MR_CLOG_FAST
+#define MR_CLOG_FAST 1
+#endif
+  const uint32_t reach = (MR_TAPE || !MR_CLOG_FAST) ? ~0u : (bit(x.conn, me) ? x.conn : 0u);
 #if MR_SEND_EARLY
   // a leader's appends read our terms at next[p] - 1: issue those loads before the applier's
   // checker stores (the ring slot is valid whatever the applier does; gated after it)
@@ -943,7 +985,7 @@ DI void node_event(const Dev& D, X& x, bool is_msg, uint32_t tnode, uint32_t slo
 #pragma unroll
   for (uint32_t p = 0; p < NB; p++) {
     const uint32_t ix = pv.nx[p] - 1u;
-    rawt[p] = (mode == SEND_APPEND && bit(peers, p) && p < D.n && ix != 0u) ? D.log[logi(D, x, me, ix)].term : 0u;
+    rawt[p] = (mode == SEND_APPEND && bit(peers & reach, p) && p < D.n && ix != 0u) ? D.log[logi(D, x, me, ix)].term : 0u;
   }
 #endif
   if (d.applied < d.commit) {  // committed entries reach the tester's applier
@@ -956,6 +998,8 @@ DI void node_event(const Dev& D, X& x, bool is_msg, uint32_t tnode, uint32_t slo
   // appends: next[p] of every peer, then the terms at next[p] - 1, as two
   // batches of independent loads, staged in LDS for the send loop
   uint64_t snapv = 0;
+  const uint32_t all = peers, seq0 = x.msgs_sent, ctr0 = d.nctr;
+  peers &= reach;
   if (mode == SEND_APPEND) {  // only a leader appends
     uint32_t nxa[NB];
     bool any_is = false;
@@ -981,9 +1025,12 @@ DI void node_event(const Dev& D, X& x, bool is_msg, uint32_t tnode, uint32_t slo
     if (any_is) snapv = NSV(me);
   }
   uint32_t plo_acc = ~0u, phi_acc = 0u;  // index range referenced by this event's payloads
-  while (peers) {  // the single send path: ascending peer order
+  while (peers) {  // the single send path: ascending peer order over the reachable peers
     uint32_t p = (uint32_t)__builtin_ctz(peers);
     peers &= peers - 1u;
+    const uint32_t below = all & ((1u << p) - 1u);  // earlier sends of this event, clogged ones too
+    x.msgs_sent = seq0 + (uint32_t)__builtin_popcount(below);
+    d.nctr = ctr0 + (uint32_t)__builtin_popcount(below);
     uint32_t st = M_RV_REQ, sa = me, sb = d.last, sc = lt, sk = 0, sinc = f_inc(d.f), prev = 0;
     uint64_t sv = 0;
     if (mode == SEND_REPLY) {
@@ -1001,7 +1048,10 @@ DI void node_event(const Dev& D, X& x, bool is_msg, uint32_t tnode, uint32_t slo
     }
     PROF(P_S_SETUP);
     int s = net_send(D, x, me, d.nctr, p, st, sinc, d.term, sa, sb, sc, sv, sk);
-    if (x.code != RUN) return;
+    if (x.code != RUN) {  // the clogged sends before this one are counted as they happened
+      CADD(CNT_DROP_CLOG, (uint32_t)__builtin_popcount(below & ~reach));
+      return;
+    }
     PROF(P_S_NET);
     if (s >= 0 && sk) {  // zero-copy payload: entries prev+1 .. prev+sk stay in this log
       plo_acc = prev + 1 < plo_acc ? prev + 1 : plo_acc;
@@ -1009,6 +1059,9 @@ DI void node_event(const Dev& D, X& x, bool is_msg, uint32_t tnode, uint32_t slo
       PROF(P_S_PAY);
     }
   }
+  x.msgs_sent = seq0 + (uint32_t)__builtin_popcount(all);  // every send of the event, clogged too
+  d.nctr = ctr0 + (uint32_t)__builtin_popcount(all);
+  CADD(CNT_DROP_CLOG, (uint32_t)__builtin_popcount(all & ~reach));
   if (plo_acc <= phi_acc) pend_note(D, x, me, d, plo_acc, phi_acc, prange.x, prange.y);
   if constexpr (KV) {
     if (kvready) {
@@ -1372,7 +1425,7 @@ __global__ void __launch_bounds__(256) reset_kernel(Dev D) {
 // cluster; out[] layout documented in mr_host.cpp (RED_*)
 __global__ void __launch_bounds__(256) reduce_kernel(Dev D, unsigned long long* out,
                                                     uint64_t cluster_base) {
-  constexpr uint32_t RN = CNT__N + 8 + 64 + 32 + 2;  // counters, scalars, verdicts, coverage, kv
+  constexpr uint32_t RN = CNT__N + 8 + 64 + 32 + 3;  // counters, scalars, verdicts, coverage, kv
   __shared__ unsigned long long acc[RN];
   for (uint32_t i = threadIdx.x; i < RN; i += blockDim.x) acc[i] = 0;
   __syncthreads();
@@ -1396,6 +1449,7 @@ __global__ void __launch_bounds__(256) reduce_kernel(Dev D, unsigned long long* 
     atomicAdd(&acc[CNT__N + 88 + bucket(CS(CS_EVENTS))], 1ull);
     atomicAdd(&acc[CNT__N + 104], (unsigned long long)CS(CS_KV_OPS));
     atomicAdd(&acc[CNT__N + 105], (unsigned long long)CS(CS_KV_CHECKED));
+    atomicAdd(&acc[CNT__N + 106], (unsigned long long)CS(CS_KV_LIN));
     if (code != RUN && code != MR_PASS)
       atomicMin(&out[CNT__N + 5], (unsigned long long)(cluster_base + x.c));
   }

@@ -14,7 +14,7 @@ import os
 import numpy as np
 
 from . import _abi
-from ._abi import EVENT_DTYPE, FAIL_NAMES, MrCfg, MrCounters, MrRunStats
+from ._abi import DECISION_DTYPE, EVENT_DTYPE, FAIL_NAMES, MrCfg, MrCounters, MrRunStats
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("MADRAFT_HIP_LIB") or os.path.join(_HERE, "lib", "libmadraft_hip.so")
@@ -48,10 +48,14 @@ def lib():
     L.mr_batch_counters.argtypes = [C.c_void_p, C.POINTER(MrCounters)]
     L.mr_trace_get.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_size_t,
                                C.POINTER(C.c_size_t)]
-    L.mr_batch_set_tape.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64]
-    L.mr_tape_get.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_size_t, C.POINTER(C.c_size_t)]
+    L.mr_batch_set_decisions.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t]
+    L.mr_batch_get_decisions.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_size_t,
+                                         C.POINTER(C.c_size_t)]
+    L.mr_decision_word.argtypes = [C.c_uint32, C.c_uint32, C.c_uint32]
+    L.mr_decision_word.restype = C.c_uint32
     L.mr_replay.argtypes = [C.POINTER(MrCfg), C.c_void_p, C.c_size_t, C.c_void_p, C.c_size_t,
-                            C.POINTER(C.c_size_t), C.POINTER(C.c_uint16), C.POINTER(C.c_uint32)]
+                            C.POINTER(C.c_size_t), C.POINTER(C.c_uint16), C.POINTER(C.c_uint32),
+                            C.POINTER(C.c_uint64)]
     L.mr_batch_destroy.argtypes = [C.c_void_p]
     L.mr_batch_destroy.restype = None
     _lib = L
@@ -166,21 +170,21 @@ class Batch:
         _check(lib().mr_batch_counters(self._b, C.byref(c)))
         return c.to_dict()
 
-    def set_tape(self, tape):
-        """Drive cluster k from tape[k] (uint32 [clusters, words], 2 words per draw;
+    def set_decisions(self, d):
+        """Drive the clusters by keyed decisions (DECISION_DTYPE records, any order;
         SEMANTICS §12); None = Philox again. Call before run()."""
-        if tape is None:
-            _check(lib().mr_batch_set_tape(self._b, None, 0))
+        if d is None or len(d) == 0:
+            _check(lib().mr_batch_set_decisions(self._b, None, 0))
             return
-        t = np.ascontiguousarray(tape, dtype=np.uint32)
-        assert t.ndim == 2 and t.shape[0] == self.clusters, t.shape
-        _check(lib().mr_batch_set_tape(self._b, t.ctypes.data, t.shape[1]))
+        a = np.ascontiguousarray(d, dtype=DECISION_DTYPE)
+        _check(lib().mr_batch_set_decisions(self._b, a.ctypes.data, a.size))
 
-    def tape(self, k, cap=1 << 20):
-        """(words drawn by cluster k, the recorded / replayed words kept, up to cap)."""
-        out = np.empty(cap, np.uint32)
+    def decisions(self, k, cap=1 << 20):
+        """(n, records): with MR_F_RECORD cluster k's decisions in draw order (n drawn);
+        with decisions set, n = its draws that found no record."""
+        out = np.empty(cap, DECISION_DTYPE)
         n = C.c_size_t()
-        _check(lib().mr_tape_get(self._b, int(k), out.ctypes.data, cap, C.byref(n)))
+        _check(lib().mr_batch_get_decisions(self._b, int(k), out.ctypes.data, cap, C.byref(n)))
         return int(n.value), out[: min(n.value, cap)]
 
     def trace(self, k, cap=None):
@@ -191,16 +195,17 @@ class Batch:
         return out[: n.value]
 
 
-def replay(test, tape, trace_cap=1 << 16, cluster_base=0, **kw):
-    """mr_replay: one cluster of `test` driven by `tape` (uint32 words, 2 per draw):
-    (per-event trace, verdict code, verdict time)."""
+def replay(test, decisions, trace_cap=1 << 16, cluster_base=0, **kw):
+    """mr_replay: one cluster of `test` driven by keyed decisions (DECISION_DTYPE records,
+    any order): (per-event trace, verdict code, verdict time, draws without a record)."""
     cfg = make_cfg(test, 1, cluster_base=cluster_base, **kw)
-    t = np.ascontiguousarray(tape, dtype=np.uint32)
+    d = np.ascontiguousarray(decisions, dtype=DECISION_DTYPE)
     out = np.empty(trace_cap, EVENT_DTYPE)
-    n, code, tm = C.c_size_t(), C.c_uint16(), C.c_uint32()
-    _check(lib().mr_replay(C.byref(cfg), t.ctypes.data, t.size, out.ctypes.data, trace_cap,
-                           C.byref(n), C.byref(code), C.byref(tm)))
-    return out[: n.value], int(code.value), int(tm.value)
+    n, code, tm, ms = C.c_size_t(), C.c_uint16(), C.c_uint32(), C.c_uint64()
+    _check(lib().mr_replay(C.byref(cfg), d.ctypes.data if d.size else None, d.size,
+                           out.ctypes.data, trace_cap, C.byref(n), C.byref(code), C.byref(tm),
+                           C.byref(ms)))
+    return out[: n.value], int(code.value), int(tm.value), int(ms.value)
 
 
 def run_test(test, seed=None, num=None, **kw):

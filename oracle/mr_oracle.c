@@ -64,9 +64,13 @@ enum { CT_QUERY = 0, CT_JOIN = 1, CT_LEAVE = 2, CT_MOVE = 3 };
 #define INF_T 0xFFFFFFFFu
 #define LOSS_Q32 429496729u /* floor(0.1 * 2^32), tester.rs:130 */
 
-/* decision tapes (SEMANTICS §12): mode 1 replays, 2 records; set by mro_set_tape */
-static uint32_t* g_tape;
-static uint64_t g_tape_words, *g_tape_used;
+/* keyed decisions (SEMANTICS §12): mode 1 replays (a sorted copy, rows by batch-relative
+ * cluster), mode 2 records in draw order; set by mro_set_decisions */
+static mr_decision* g_dec;       /* mode 1: sorted by (cluster, stream, entity, seq) */
+static uint64_t* g_dec_off;      /* mode 1: row r = g_dec[g_dec_off[r] .. g_dec_off[r + 1]) */
+static uint64_t g_dec_rows;
+static mr_decision* g_rec;       /* mode 2: [rows][g_rec_cap] */
+static uint64_t g_rec_cap, *g_dec_count;
 static int g_tape_mode;
 
 static inline uint32_t u_range(uint32_t w, uint32_t lo, uint32_t hi) {
@@ -101,6 +105,7 @@ typedef struct {
   uint32_t id, lh, seq, tag, nctr, waiting, got, rstat, rhint, rval; uint64_t rvh;
   uint32_t owner, mcl; /* the thread its calls wake (0 = the test body); mcl: a test-body clerk */
   uint32_t op, key, elem;
+  uint32_t llo; /* a Get's lower bound at its call (SEMANTICS §9a) */
 } OClerk;
 typedef struct {
   uint32_t tid, live, pc, j, cli, tctr, gen;
@@ -136,7 +141,7 @@ typedef struct {
   HEnt* heap; uint32_t heap_n, heap_cap;
   /* tester */
   uint32_t t_ctr;
-  uint8_t* mask; uint64_t* sval; uint32_t slen[MR_MAX_NODES];
+  uint8_t* mask; uint64_t* sval; uint32_t* sterm; uint32_t slen[MR_MAX_NODES];
   /* kvraft (SEMANTICS §8-9) */
   uint32_t kv_mode, kv_done, next_tid, mwake, main_join;
   OKey kv[MR_MAX_NODES][KV_KEYS]; uint32_t kv_dedup[MR_MAX_NODES][MAX_CLERKS];
@@ -147,9 +152,11 @@ typedef struct {
   OClerk ck[CK_SLOTS]; OThr th[MAX_THR];
   uint64_t* cval; uint32_t* cidx; /* churn values [3][CHURN_VCAP] + their indices */
   uint32_t ctrl_mode, nops, ncfg[MR_MAX_NODES];
-  uint32_t lring[32]; /* MR_F_SAFETY: (term << 4) | leader + 1 by term mod 32 */
+  uint32_t led[64];   /* MR_F_SAFETY: bit t = a leader was elected in term t (t < 2048) */
+  uint32_t lin[KV_KEYS][KV_APP][5]; /* linearizability: per (key, appender) tag, called, acked,
+                                     * seen, and a pending all-appenders Get's lower bound */
   uint8_t link[MR_MAX_NODES]; /* server links (connect2/disconnect2): bit j of link[i] = i~j */
-  uint32_t* tape_row; uint64_t tape_pos; /* decision tape of this cluster (SEMANTICS §12) */
+  uint64_t tape_row; int tape_on; uint64_t tape_pos; /* keyed decisions: row, count (§12) */
   uint8_t ccut[CK_SLOTS];     /* clerk links cut: bit j of ccut[k] = clerk host 8 + k !~ server j */
   OCfg* cfgs; /* [MR_MAX_NODES][CFG_CAP] */
   OOp* ops;   /* [OP_CAP] */
@@ -242,20 +249,35 @@ static void set_timer(OSim* s, uint32_t d, uint32_t t) {
   heap_push(s, ((uint64_t)t << 32) | (1ull << 30) | d, d, x->timer_gen);
 }
 
-/* every random draw of the simulation: Philox4x32-10 keyed by the seed (§2), or the tape */
+static int dec_cmp(const mr_decision* a, uint32_t stream, uint32_t entity, uint32_t seq) {
+  if (a->stream != stream) return a->stream < stream ? -1 : 1;
+  if (a->entity != entity) return a->entity < entity ? -1 : 1;
+  if (a->seq != seq) return a->seq < seq ? -1 : 1;
+  return 0;
+}
+
+/* every random draw of the simulation: Philox4x32-10 with counter (seq, entity, stream)
+ * keyed by the seed (§2), or the keyed decision recorded for (stream, entity, seq) (§12) */
 static void draw(OSim* s, const uint32_t ctr[4], uint32_t w[4]) {
-  uint64_t p = s->tape_pos;
-  if (s->tape_row && g_tape_mode == 1) {
-    s->tape_pos = p + 2;
-    w[0] = p < g_tape_words ? s->tape_row[p] : 0u;
-    w[1] = p + 1 < g_tape_words ? s->tape_row[p + 1] : 0u;
-    w[2] = w[3] = 0;
-    return;
+  if (s->tape_on && g_tape_mode == 1) {
+    const mr_decision* row = g_dec + g_dec_off[s->tape_row];
+    uint64_t lo = 0, hi = g_dec_off[s->tape_row + 1] - g_dec_off[s->tape_row];
+    while (lo < hi) { /* binary search of the row */
+      uint64_t mid = (lo + hi) / 2;
+      int c = dec_cmp(&row[mid], ctr[2], ctr[1], ctr[0]);
+      if (c == 0) { w[0] = row[mid].w0; w[1] = row[mid].w1; w[2] = w[3] = 0; return; }
+      if (c < 0) lo = mid + 1; else hi = mid;
+    }
+    s->tape_pos++; /* no record: the seed's own draw */
   }
   mro_philox4x32_10(ctr, s->key, w);
-  if (s->tape_row && g_tape_mode == 2) {
-    s->tape_pos = p + 2;
-    if (p + 1 < g_tape_words) { s->tape_row[p] = w[0]; s->tape_row[p + 1] = w[1]; }
+  if (s->tape_on && g_tape_mode == 2) {
+    uint64_t p = s->tape_pos++;
+    if (p < g_rec_cap) {
+      mr_decision* r = &g_rec[s->tape_row * g_rec_cap + p];
+      r->cluster = (uint32_t)s->tape_row; r->stream = (uint16_t)ctr[2];
+      r->entity = (uint16_t)ctr[1]; r->seq = ctr[0]; r->w0 = w[0]; r->w1 = w[1];
+    }
   }
 }
 
@@ -283,11 +305,16 @@ static uint32_t* host_nctr(OSim* s, uint32_t h) {
   if (h < CLERK_HOST) return &s->nd[h].n_ctr;
   return &s->ck[h - CLERK_HOST].nctr;
 }
+/* the sender's identity in its NET draws (§2, §12): server i, or clerk id k as 8 + k (a
+ * clerk's host slot is reused by later clerks; its id, like madsim's 0.0.2.id address, is not) */
+static uint32_t host_entity(OSim* s, uint32_t h) {
+  return h < CLERK_HOST ? h : CLERK_HOST + s->ck[h - CLERK_HOST].id;
+}
 
 static void net_send(OSim* s, uint32_t src, uint32_t dst, OMsg* m) {
   uint32_t seq = (uint32_t)s->r.msgs_sent;
   s->r.msgs_sent++;
-  uint32_t ctr[4] = {(*host_nctr(s, src))++, src, ST_NET, 0}, w[4];
+  uint32_t ctr[4] = {(*host_nctr(s, src))++, host_entity(s, src), ST_NET, 0}, w[4];
   draw(s, ctr, w);
   if (!host_conn(s, src) || !host_conn(s, dst) || !link_up(s, src, dst)) { s->r.drop_clog++; return; }
   if (w[0] < s->loss) { s->r.drop_loss++; return; }
@@ -306,13 +333,14 @@ static void net_send(OSim* s, uint32_t src, uint32_t dst, OMsg* m) {
 /* ------------------------------------------------------------------ */
 /* tester storage (tester.rs:366-428)                                   */
 /* ------------------------------------------------------------------ */
-static void push_and_check(OSim* s, uint32_t i, uint32_t idx, uint64_t v) {
+static void push_and_check(OSim* s, uint32_t i, uint32_t idx, uint64_t v, uint32_t term) {
   if (idx >= s->cfg.apply_cap) t_fail(s, MR_FAIL_SIM_CAPACITY);
   s->r.applies++;
   if (s->mask[idx] && s->sval[idx] != v) t_fail(s, MR_FAIL_APPLY_MISMATCH); /* :384 */
   if (idx > s->slen[i]) t_fail(s, MR_FAIL_APPLY_OUT_OF_ORDER);              /* :393 */
   if (idx == s->slen[i]) {
     s->sval[idx] = v;
+    s->sterm[idx] = term;
     s->mask[idx] |= (uint8_t)(1u << i);
     s->slen[i]++;
     if (idx > s->r.max_index) s->r.max_index = idx;
@@ -433,8 +461,20 @@ static uint32_t put_len(uint32_t t) { return t == 0 ? 0 : t < (1u << 20) ? ndig(
 /* the state of appender `cli` of a key: count | ok << 31 (ok: its tokens arrived in order, once) */
 static uint32_t kv_app_state(const OKey* k, uint32_t cli) {
   for (uint32_t a = 0; a < KV_APP; a++)
-    if ((k->app[a] & 0xFFu) == cli + 1) return ((k->app[a] >> 8) & 0xFFFFFFu) | ((~k->app[a] >> 31) << 31);
+    if ((k->app[a] & 0xFFu) == cli + 1) return ((k->app[a] >> 8) & 0x7FFFFFu) | ((~k->app[a] >> 31) << 31);
   return 1u << 31;
+}
+
+/* a Get's reply value: the state of appender elem, or (KV_ALL) of appenders 0..4 packed as
+ * count (5 bits, saturating at 31) | ok << 5 each */
+static uint32_t kv_get_value(const OKey* k, uint32_t elem) {
+  if (elem != KV_ALL) return kv_app_state(k, elem);
+  uint32_t out = 0;
+  for (uint32_t c = 0; c < KV_APP; c++) {
+    uint32_t st = kv_app_state(k, c), n = st & 0xFFFFFFu;
+    out |= ((n > 31 ? 31 : n) | ((st >> 31) ? 32u : 0u)) << (6 * c);
+  }
+  return out;
 }
 
 /* Kv::apply (kvraft/server.rs:74-87, the build's completion; SEMANTICS §9) of log entry i
@@ -451,15 +491,8 @@ static void kv_apply(OSim* s, uint32_t me, uint32_t i, uint64_t v) {
     query = s->ops[elem].type == CT_QUERY;
   } else if (op == KV_GET) {
     outh = k->h;
-    if (elem == KV_ALL) { /* appenders 0..4: count (5 bits) | ok << 5 each */
-      for (uint32_t c = 0; c < KV_APP; c++) {
-        uint32_t st = kv_app_state(k, c), n = st & 0xFFFFFFu;
-        out |= ((n > 31 ? 31 : n) | ((n <= 31 && (st >> 31)) ? 32u : 0u)) << (6 * c);
-      }
-    } else {
-      out = kv_app_state(k, elem);
-    }
-  } else if (seq > s->kv_dedup[me][clerk]) {
+    out = kv_get_value(k, elem);
+  } else if (seq > s->kv_dedup[me][clerk] || (s->cfg.flags & MR_F_BUG_NO_DEDUP)) {
     if (op == KV_PUT) { /* elem = the value's token (0 = "") */
       memset(k, 0, sizeof *k);
       if (elem) { k->h = (elem + 1ull) * 0x9E3779B97F4A7C15ull; k->len = put_len(elem); }
@@ -565,7 +598,7 @@ static void node_apply(OSim* s, uint32_t me) {
   while (d->applied < d->commit) {
     uint32_t i = ++d->applied;
     uint64_t v = d->lval[lpos(s, i)];
-    push_and_check(s, me, i, v);
+    push_and_check(s, me, i, v, d->lterm[lpos(s, i)]);
     if (s->kv_mode) kv_apply(s, me, i, v);
     if (s->kv_maxraft && i % KV_SNAP_EVERY == 0 && i > d->snap_idx &&
         raft_state_size(d) >= s->kv_maxraft / 2) kv_snapshot(s, me, i);
@@ -598,15 +631,19 @@ static void send_append(OSim* s, uint32_t me, uint32_t p) {
   net_send(s, me, p, &m);
 }
 
-/* MR_F_SAFETY (SEMANTICS §11): election safety over a ring of the last 32 terms'
- * leaders, and leader completeness for the highest index any server applied */
+/* MR_F_SAFETY (SEMANTICS §11) when `me` wins its term: election safety, exact (one bit
+ * per term that had a leader), and leader completeness for the committed entry at the
+ * highest index any server applied (index, term and command; log matching, checked at
+ * every AppendEntries, extends it to every earlier committed entry) */
 static void safety_on_leader(OSim* s, uint32_t me) {
   ONode* d = &s->nd[me];
-  uint32_t t = d->term, e = s->lring[t & 31u];
-  if ((e >> 4) == t && (e & 15u) != me + 1) t_fail(s, MR_FAIL_SAFETY_ELECTION);
-  s->lring[t & 31u] = (t << 4) | (me + 1);
+  uint32_t t = d->term;
+  if (t >= 64u * 32u) t_fail(s, MR_FAIL_SIM_CAPACITY);
+  if ((s->led[t >> 5] >> (t & 31u)) & 1u) t_fail(s, MR_FAIL_SAFETY_ELECTION);
+  s->led[t >> 5] |= 1u << (t & 31u);
   uint32_t j = (uint32_t)s->r.max_index;
-  if (j > d->snap_idx && (j > d->last || d->lval[lpos(s, j)] != s->sval[j]))
+  if (j > d->snap_idx && (j > d->last || d->lval[lpos(s, j)] != s->sval[j] ||
+                          d->lterm[lpos(s, j)] != s->sterm[j]))
     t_fail(s, MR_FAIL_SAFETY_COMPLETENESS);
 }
 
@@ -690,6 +727,13 @@ static void kv_request(OSim* s, uint32_t me, OMsg* m) {
   if (s->null_raft) t_fail(s, MR_FAIL_TODO_APPLY);
   if (d->role != R_L) {
     kv_send_rep(s, me, m->src, clerk, m->term, KV_WRONG_LEADER, (me + 1) % s->n, 0, 0);
+    return;
+  }
+  if ((s->cfg.flags & MR_F_BUG_STALE_READ) && (m->a & 3u) == KV_GET && !s->ctrl_mode) {
+    /* the buggy leader answers from its own state at once: no log entry, no quorum */
+    OKey* k = &s->kv[me][(m->a >> 2) & 63u];
+    uint32_t elem = m->c & 0xFFFFFFu;
+    kv_send_rep(s, me, m->src, clerk, m->term, KV_OK, me, kv_get_value(k, elem), k->h);
     return;
   }
   uint32_t p = 0;
@@ -1457,9 +1501,63 @@ static void clerk_send(OSim* s, uint32_t slot) { /* one call_timeout attempt, cl
   thr_wake(s, c->owner, s->now + 500000u); /* Duration::from_millis(500) */
 }
 
+/* ---- the linearizability checker (SEMANTICS §9a): each key is an append / get register;
+ * per (key, appender) the tester counts the appends called and acknowledged and the largest
+ * count a returned Get observed, and bounds every Get's observed count by the call / return
+ * order: at least the appends acknowledged (and the count seen by Gets that returned) before
+ * it was called, at most the appends called before it returned, and the appender's tokens in
+ * order, once each. */
+static uint32_t* lin_ent(OSim* s, uint32_t key, uint32_t cli) {
+  key &= KV_KEYS - 1; /* the key as the command carries it (6 bits, kv_request) */
+  for (uint32_t a = 0; a < KV_APP; a++) {
+    uint32_t* e = s->lin[key][a];
+    if (e[0] == cli + 1) return e;
+    if (e[0] == 0) { e[0] = cli + 1; e[1] = e[2] = e[3] = e[4] = 0; return e; }
+  }
+  t_fail(s, MR_FAIL_SIM_CAPACITY);
+  return NULL;
+}
+static void lin_call(OSim* s, OClerk* c) {
+  if (s->ctrl_mode) return;
+  if (c->op == KV_PUT) { /* a new value */
+    memset(s->lin[c->key & (KV_KEYS - 1)], 0, sizeof s->lin[0]);
+    return;
+  }
+  if (c->op == KV_APPEND) { lin_ent(s, c->key, c->elem >> 19)[1]++; return; }
+  if (c->elem == KV_ALL) { /* appenders 0..4: each one's bound, kept in its entry */
+    for (uint32_t cli = 0; cli < KV_APP; cli++) {
+      uint32_t* e = lin_ent(s, c->key, cli);
+      e[4] = e[2] > e[3] ? e[2] : e[3];
+    }
+    return;
+  }
+  uint32_t* e = lin_ent(s, c->key, c->elem);
+  c->llo = e[2] > e[3] ? e[2] : e[3];
+}
+static void lin_return(OSim* s, OClerk* c) {
+  if (s->ctrl_mode) return;
+  if (c->op == KV_APPEND) { lin_ent(s, c->key, c->elem >> 19)[2]++; return; }
+  if (c->op != KV_GET) return;
+  if (c->elem == KV_ALL) { /* count (5 bits, 31 = saturated) | ok << 5 per appender */
+    s->r.kv_lin_checked++;
+    for (uint32_t cli = 0; cli < KV_APP; cli++) {
+      uint32_t* e = lin_ent(s, c->key, cli), st = (c->rval >> (6 * cli)) & 63u, n = st & 31u;
+      if (!(st >> 5) || (n < 31u && (n < e[4] || n > e[1]))) t_fail(s, MR_FAIL_KV_NOT_LINEARIZABLE);
+      if (n > e[3]) e[3] = n;
+    }
+    return;
+  }
+  uint32_t* e = lin_ent(s, c->key, c->elem);
+  uint32_t n = c->rval & 0xFFFFFFu;
+  s->r.kv_lin_checked++;
+  if (!(c->rval >> 31) || n < c->llo || n > e[1]) t_fail(s, MR_FAIL_KV_NOT_LINEARIZABLE);
+  if (n > e[3]) e[3] = n;
+}
+
 static void clerk_begin(OSim* s, uint32_t slot, uint32_t op, uint32_t key, uint32_t elem) {
   OClerk* c = &s->ck[slot];
   c->seq++; c->op = op; c->key = key; c->elem = elem;
+  lin_call(s, c);
   clerk_send(s, slot);
 }
 
@@ -1470,7 +1568,7 @@ static int clerk_resume(OSim* s, uint32_t slot) {
   /* the as-shipped ClerkCore::call: todo!() once call_timeout returns (kvraft/client.rs:59) */
   if (s->null_raft) t_fail(s, MR_FAIL_TODO_RPC_RESULTS);
   if (c->got) {
-    if (c->rstat == KV_OK) { s->r.kv_ops++; return 1; }
+    if (c->rstat == KV_OK) { s->r.kv_ops++; lin_return(s, c); return 1; }
     c->lh = c->rstat == KV_WRONG_LEADER ? c->rhint : (c->lh + 1) % s->n;
   } else {
     c->lh = (c->lh + 1) % s->n;
@@ -2329,12 +2427,13 @@ static int sim_alloc(OSim* s, const mr_cfg* cfg) {
   s->kring_idx = (uint32_t*)malloc(KV_RING * sizeof(uint32_t));
   s->mask = (uint8_t*)malloc(cfg->apply_cap);
   s->sval = (uint64_t*)malloc(cfg->apply_cap * sizeof(uint64_t));
+  s->sterm = (uint32_t*)malloc(cfg->apply_cap * sizeof(uint32_t));
   return 0;
 }
 
 static void sim_free(OSim* s) {
   for (uint32_t i = 0; i < MR_MAX_NODES; i++) { free(s->nd[i].lterm); free(s->nd[i].lval); }
-  free(s->mask); free(s->sval); free(s->heap); free(s->cval); free(s->cidx);
+  free(s->mask); free(s->sval); free(s->sterm); free(s->heap); free(s->cval); free(s->cidx);
   free(s->cfgs); free(s->ops); free(s->kvs); free(s->kring); free(s->kring_idx);
 }
 
@@ -2360,7 +2459,8 @@ static void sim_reset(OSim* s, uint64_t cluster) {
   memset(s->kv_dedup, 0, sizeof s->kv_dedup); memset(s->pend, 0, sizeof s->pend);
   memset(s->ck, 0, sizeof s->ck); memset(s->th, 0, sizeof s->th); s->churn_stop = 0;
   s->ctrl_mode = 0; s->nops = 0;
-  memset(s->lring, 0, sizeof s->lring);
+  memset(s->led, 0, sizeof s->led);
+  memset(s->lin, 0, sizeof s->lin);
   s->kv_maxraft = 0;
   memset(s->kvs, 0, MR_MAX_NODES * sizeof(OKvState));
   memset(s->kring_idx, 0, KV_RING * sizeof(uint32_t));
@@ -2376,7 +2476,8 @@ static void sim_reset(OSim* s, uint64_t cluster) {
   s->r.digest = 0xCBF29CE484222325ull;
   s->n_trace = 0;
   uint64_t row = cluster - s->cfg.cluster_base;
-  s->tape_row = g_tape_mode ? g_tape + row * g_tape_words : NULL;
+  s->tape_row = row;
+  s->tape_on = g_tape_mode == 2 || (g_tape_mode == 1 && row < g_dec_rows);
   s->tape_pos = 0;
 }
 
@@ -2387,11 +2488,40 @@ static void sim_run(OSim* s, uint64_t cluster) {
     s->r.ev_tester++;
     if (run_scenario(s) != 0) t_fail(s, MR_FAIL_SIM_BAD_PROGRAM);
   }
-  if (g_tape_mode && g_tape_used) g_tape_used[cluster - s->cfg.cluster_base] = s->tape_pos;
+  if (s->tape_on && g_dec_count) g_dec_count[cluster - s->cfg.cluster_base] = s->tape_pos;
 }
 
-void mro_set_tape(uint32_t* tape, uint64_t words_per_cluster, int mode, uint64_t* used) {
-  g_tape = tape; g_tape_words = words_per_cluster; g_tape_mode = tape ? mode : 0; g_tape_used = used;
+static int dec_sort(const void* a, const void* b) {
+  const mr_decision* x = (const mr_decision*)a;
+  const mr_decision* y = (const mr_decision*)b;
+  if (x->cluster != y->cluster) return x->cluster < y->cluster ? -1 : 1;
+  return dec_cmp(x, y->stream, y->entity, y->seq);
+}
+
+int mro_set_decisions(int mode, const mr_decision* d, uint64_t n, uint64_t rows,
+                      mr_decision* rec, uint64_t rec_cap, uint64_t* count) {
+  free(g_dec); free(g_dec_off);
+  g_dec = NULL; g_dec_off = NULL; g_dec_rows = 0; g_rec = NULL; g_rec_cap = 0;
+  g_dec_count = count; g_tape_mode = 0;
+  if (mode == 1) {
+    g_dec = (mr_decision*)malloc((n ? n : 1) * sizeof(mr_decision));
+    g_dec_off = (uint64_t*)calloc(rows + 1, sizeof(uint64_t));
+    if (n) memcpy(g_dec, d, n * sizeof(mr_decision));
+    qsort(g_dec, n, sizeof(mr_decision), dec_sort);
+    for (uint64_t i = 0; i < n; i++) {
+      if (g_dec[i].cluster >= rows) return -1;
+      if (i && g_dec[i].cluster == g_dec[i - 1].cluster &&
+          dec_cmp(&g_dec[i], g_dec[i - 1].stream, g_dec[i - 1].entity, g_dec[i - 1].seq) == 0)
+        return -2; /* duplicate key */
+      g_dec_off[g_dec[i].cluster + 1]++;
+    }
+    for (uint64_t r = 0; r < rows; r++) g_dec_off[r + 1] += g_dec_off[r];
+    g_dec_rows = rows;
+  } else if (mode == 2) {
+    g_rec = rec; g_rec_cap = rec_cap;
+  }
+  g_tape_mode = mode;
+  return 0;
 }
 
 int mro_run_cluster(const mr_cfg* cfg, uint64_t cluster, mro_result* out, mr_event* trace,
@@ -2418,7 +2548,7 @@ static void acc(mro_result* a, const mro_result* b) {
   if (b->max_inflight > a->max_inflight) a->max_inflight = b->max_inflight;
   if (b->max_log > a->max_log) a->max_log = b->max_log;
   if (b->max_index > a->max_index) a->max_index = b->max_index;
-  a->kv_ops += b->kv_ops; a->kv_checked += b->kv_checked;
+  a->kv_ops += b->kv_ops; a->kv_checked += b->kv_checked; a->kv_lin_checked += b->kv_lin_checked;
 }
 
 int mro_run_batch(const mr_cfg* cfg, uint64_t first, uint64_t count, uint16_t* code,
@@ -2521,6 +2651,7 @@ const char* mro_fail_message(uint32_t code) {
     case MR_FAIL_SAFETY_LOG_MATCHING: return "log matching: same index and term, different entries";
     case MR_FAIL_TODO_APPLY: return "not yet implemented: apply command";
     case MR_FAIL_TODO_RPC_RESULTS: return "not yet implemented: handle RPC results";
+    case MR_FAIL_KV_NOT_LINEARIZABLE: return "history is not linearizable";
     case MR_FAIL_SIM_CAPACITY: return "simulator capacity exceeded";
     case MR_FAIL_SIM_EVENT_LIMIT: return "simulator event limit exceeded";
     default: return "scenario assertion failed";

@@ -37,6 +37,7 @@ typedef struct mro_result {
   uint64_t kv_ops;      /* service clerk calls completed (kvraft / shard_ctrler) */
   uint64_t kv_checked;  /* Get results the tester verified against their linearizable value */
   uint64_t log_writes;  /* log entries written (leader appends + follower appends) */
+  uint64_t kv_lin_checked; /* Gets the linearizability checker verified (SEMANTICS §9a) */
 } mro_result;
 
 /* Run cluster `cluster` (global id) of cfg; trace (optional) receives up to
@@ -49,10 +50,12 @@ int mro_run_batch(const mr_cfg* cfg, uint64_t first, uint64_t count,
                   uint16_t* code, uint32_t* time_us, uint64_t* digest,
                   mro_result* sum);
 
-/* Decision tapes (SEMANTICS §12) for the following runs: mode 1 replays tape row
- * (cluster - cfg.cluster_base), mode 2 records into it; used[row] = words drawn. NULL = off.
- * Not thread-safe (one tape per process). */
-void mro_set_tape(uint32_t* tape, uint64_t words_per_cluster, int mode, uint64_t* used);
+/* Keyed decisions (SEMANTICS §12) for the following runs, rows = cluster - cfg.cluster_base:
+ * mode 1 replays the n decisions `d` (any order; rows >= every d.cluster + 1), count[row] =
+ * draws without a record; mode 2 records every draw into rec[row * rec_cap ..] in draw order,
+ * count[row] = draws; mode 0 = off. Returns <0 on a bad / duplicate record. Not thread-safe. */
+int mro_set_decisions(int mode, const mr_decision* d, uint64_t n, uint64_t rows,
+                      mr_decision* rec, uint64_t rec_cap, uint64_t* count);
 
 /* Philox4x32-10 block (exported for the known-answer test). */
 void mro_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]);

@@ -8,7 +8,7 @@ import os
 
 import numpy as np
 
-from madraft_amd._abi import EVENT_DTYPE, MrCfg
+from madraft_amd._abi import DECISION_DTYPE, EVENT_DTYPE, MrCfg
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB = os.path.join(ROOT, "oracle", "_build", "libmr_oracle.so")
@@ -20,7 +20,7 @@ class MroResult(C.Structure):
             "events", "ev_msg", "ev_timer", "ev_tester", "msgs_sent", "drop_clog", "drop_loss",
             "drop_overflow", "drop_deliver", "drop_stale", "elections", "leaders_elected",
             "applies", "snapshots", "installs", "entries_shipped", "max_inflight", "max_log",
-            "max_index", "kv_ops", "kv_checked", "log_writes")]
+            "max_index", "kv_ops", "kv_checked", "log_writes", "kv_lin_checked")]
 
     def to_dict(self):
         return {n: int(getattr(self, n)) for n, _ in self._fields_}
@@ -40,8 +40,8 @@ class Oracle:
                                         C.POINTER(C.c_uint32 * 4)]
         L.mro_philox4x32_10.restype = None
         L.mro_cfg_init.argtypes = [C.POINTER(MrCfg), C.c_uint32]
-        L.mro_set_tape.argtypes = [C.c_void_p, C.c_uint64, C.c_int, C.c_void_p]
-        L.mro_set_tape.restype = None
+        L.mro_set_decisions.argtypes = [C.c_int, C.c_void_p, C.c_uint64, C.c_uint64, C.c_void_p,
+                                        C.c_uint64, C.c_void_p]
         L.mro_scenario_from_name.argtypes = [C.c_char_p]
         L.mro_scenario_from_name.restype = C.c_uint32
         self.L = L
@@ -75,20 +75,39 @@ class Oracle:
         assert rc == 0, "bad config"
         return r.to_dict(), tr[: min(n.value, trace_cap)] if trace_cap else None
 
-    def with_tape(self, tape, mode):
-        """Context: the following runs replay (mode 1) or record into (mode 2) `tape`
-        (uint32 [clusters, words], row = cluster - cfg.cluster_base); yields words drawn."""
+    def recording(self, rows, cap):
+        """Context: the following runs record every draw as a keyed decision (SEMANTICS §12);
+        yields (count[rows], rec[rows, cap]) with row = cluster - cfg.cluster_base."""
         import contextlib
 
         @contextlib.contextmanager
         def ctx():
-            used = np.zeros(tape.shape[0], np.uint64)
-            self.L.mro_set_tape(tape.ctypes.data, tape.shape[1], mode, used.ctypes.data)
+            count = np.zeros(rows, np.uint64)
+            rec = np.zeros((rows, cap), DECISION_DTYPE)
+            assert self.L.mro_set_decisions(2, None, 0, rows, rec.ctypes.data, cap,
+                                            count.ctypes.data) == 0
             try:
-                yield used
+                yield count, rec
             finally:
-                self.L.mro_set_tape(None, 0, 0, None)
-        assert tape.dtype == np.uint32 and tape.flags.c_contiguous
+                self.L.mro_set_decisions(0, None, 0, 0, None, 0, None)
+        return ctx()
+
+    def replaying(self, decisions, rows):
+        """Context: the following runs take their draws from `decisions` (DECISION_DTYPE,
+        any order, cluster = row); yields misses[rows] (draws without a record)."""
+        import contextlib
+
+        @contextlib.contextmanager
+        def ctx():
+            d = np.ascontiguousarray(decisions, dtype=DECISION_DTYPE)
+            misses = np.zeros(rows, np.uint64)
+            rc = self.L.mro_set_decisions(1, d.ctypes.data if d.size else None, d.size, rows,
+                                          None, 0, misses.ctypes.data)
+            assert rc == 0, rc
+            try:
+                yield misses
+            finally:
+                self.L.mro_set_decisions(0, None, 0, 0, None, 0, None)
         return ctx()
 
     def run_batch(self, cfg, first, count):

@@ -20,7 +20,8 @@ SUPPORTED = [n for n in _abi.SCENARIOS if n and n not in _abi.GPU_UNSUPPORTED]
 COUNTER_KEYS = ["events", "ev_msg", "ev_timer", "ev_tester", "msgs_sent", "drop_clog",
                 "drop_loss", "drop_overflow", "drop_deliver", "drop_stale", "elections",
                 "leaders_elected", "applies", "snapshots", "installs", "entries_shipped",
-                "max_inflight", "max_log", "max_index", "kv_ops", "kv_checked", "log_writes"]
+                "max_inflight", "max_log", "max_index", "kv_ops", "kv_checked", "log_writes",
+                "kv_lin_checked"]
 
 
 def first_diff(a, b):
@@ -167,6 +168,19 @@ def test_safety_checks_bit_exact(hip, oracle, test, flags):
         assert (code != 0).sum() >= 10
     else:
         assert not np.isin(code, [42, 43, 49]).any()
+
+
+@pytest.mark.parametrize("test,flags", [
+    ("unreliable_3a", _abi.MR_F_BUG_NO_DEDUP),
+    ("unreliable_one_key_3a", _abi.MR_F_BUG_NO_DEDUP),
+    ("persist_partition_unreliable_3a", _abi.MR_F_BUG_STALE_READ),
+    ("many_partitions_many_clients_3a", _abi.MR_F_BUG_STALE_READ),
+])
+def test_linearizability_checker_bit_exact(hip, oracle, test, flags):
+    """SEMANTICS §9a on the GPU: the buggy kvraft servers are caught at the same Get, at the
+    same virtual time, with the same traces and counters as the oracle."""
+    code, cnt = compare(hip, oracle, test, 256, flags=flags)
+    assert (code == 52).sum() >= 10 and cnt["kv_lin_checked"] > 0
 
 
 @pytest.mark.parametrize("test", ["figure_8_unreliable_2c", "unreliable_3a"])

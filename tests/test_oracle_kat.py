@@ -174,3 +174,27 @@ def test_safety_catches_buggy_raft(oracle, bug, test, code_):
     assert (code == code_).sum() >= 10
     plain, *_ = oracle.run_batch(oracle.cfg(test, flags=bug), 0, 200)
     assert (plain != 0).sum() >= 9
+
+
+@pytest.mark.parametrize("test", _abi.KV_TESTS)
+def test_linearizability_checker_accepts_correct_runs(oracle, test):
+    """SEMANTICS §9a: every Get of every kvraft test is bounded by its call / return order
+    and passes on the completed server (no false alarm on 16 seeds)."""
+    code, _, _, s = oracle.run_batch(oracle.cfg(test), 0, 16)
+    assert (code == 0).all()
+    assert s["kv_lin_checked"] >= s["kv_checked"] > 0
+
+
+@pytest.mark.parametrize("bug,test,min_hits", [
+    (_abi.MR_F_BUG_NO_DEDUP, "unreliable_3a", 60),                     # retried appends twice
+    (_abi.MR_F_BUG_NO_DEDUP, "unreliable_one_key_3a", 60),             # ... seen by the final Get
+    (_abi.MR_F_BUG_NO_DEDUP, "snapshot_unreliable_recover_concurrent_partition_3b", 60),
+    (_abi.MR_F_BUG_STALE_READ, "persist_partition_unreliable_3a", 60),  # deposed leader reads
+    (_abi.MR_F_BUG_STALE_READ, "many_partitions_many_clients_3a", 10),
+])
+def test_linearizability_checker_catches_buggy_servers(oracle, bug, test, min_hits):
+    """A kvraft server without per-clerk dedup re-applies retried appends, and one whose
+    leader answers Gets from its own state returns stale values after a partition: the
+    checker flags both (KV_NOT_LINEARIZABLE, 52) at the offending Get."""
+    code, *_ = oracle.run_batch(oracle.cfg(test, flags=bug), 0, 64)
+    assert (code == 52).sum() >= min_hits, {int(c): int((code == c).sum()) for c in np.unique(code)}
