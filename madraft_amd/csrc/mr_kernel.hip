@@ -328,7 +328,7 @@ DI void reset_timer(const Dev& D, X& x, uint32_t d, NC& n) {  // raft.rs:260-263
 }
 
 #ifndef MR_RESCAN_OCC  // scan only the occupied slots (A/B: DESIGN.md §6)
-#define MR_RESCAN_OCC 0
+#define MR_RESCAN_OCC 1
 #endif
 DI void rescan_min(const Dev& D, X& x) {
   uint64_t best = ~0ull;
