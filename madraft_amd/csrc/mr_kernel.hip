@@ -87,7 +87,17 @@ struct X {
 // ~0, so the earliest-message scan is a branch-free min over all M slots.
 // lanes per block: 128, or 64 where 256 slots of keys must fit the 160 KiB of LDS
 constexpr uint32_t STEP_BLOCK = MW > 2 ? 64 : 128;
-extern __shared__ uint64_t s_keys[];
+// MR_KEY32: a 32-bit LDS key t << 5 | dst (t < 2^27 - 1, SEMANTICS §4); the (rare) tie of
+// two messages at the same t is broken by their sequence numbers, kept in the message
+// record (word MF_PAD). Otherwise a 64-bit key (t << 32 | seq << 5 | dst).
+#ifndef MR_KEY32
+#define MR_KEY32 0
+#endif
+using lkey_t = std::conditional_t<MR_KEY32 != 0, uint32_t, uint64_t>;
+constexpr lkey_t LKEY_FREE = ~lkey_t(0);
+constexpr uint32_t T_KEY_MAX = (1u << 27) - 1u;  // delivery times at or past it: SIM_CAPACITY
+extern __shared__ uint64_t s_keys_raw[];
+#define s_keys reinterpret_cast<lkey_t*>(s_keys_raw)
 #define LK(s) s_keys[(s) * STEP_BLOCK + threadIdx.x]
 // send-loop staging after the M keys: next[p] and term at next[p] - 1 (u32)
 #define LNX(p) reinterpret_cast<uint32_t*>(s_keys + D.M * STEP_BLOCK)[(p) * STEP_BLOCK + threadIdx.x]
@@ -331,6 +341,40 @@ DI void reset_timer(const Dev& D, X& x, uint32_t d, NC& n) {  // raft.rs:260-263
 #define MR_RESCAN_OCC 1
 #endif
 DI void rescan_min(const Dev& D, X& x) {
+  if constexpr (MR_KEY32) {
+    uint32_t bt = ~0u, bk = ~0u, bs = 0;
+    bool tie = false;
+#pragma unroll
+    for (uint32_t w = 0; w < MW; w++) {
+      const uint32_t mw = D.M > 64u * w ? D.M - 64u * w : 0u;
+      uint64_t occ = ~x.free_mask[w] & (mw >= 64 ? ~0ull : ((1ull << mw) - 1ull));
+      while (occ) {
+        const uint32_t s = 64u * w + (uint32_t)__builtin_ctzll(occ);
+        occ &= occ - 1ull;
+        const uint32_t k = (uint32_t)LK(s), t = k >> 5;
+        tie = t == bt || (tie && t > bt);
+        if (t < bt) { bt = t; bk = k; bs = s; }
+      }
+    }
+    if (tie) {  // two or more messages at time bt: the smaller sequence number first
+      uint32_t bq = ~0u;
+      for (uint32_t w = 0; w < MW; w++) {
+        const uint32_t mw = D.M > 64u * w ? D.M - 64u * w : 0u;
+        uint64_t occ = ~x.free_mask[w] & (mw >= 64 ? ~0ull : ((1ull << mw) - 1ull));
+        while (occ) {
+          const uint32_t s = 64u * w + (uint32_t)__builtin_ctzll(occ);
+          occ &= occ - 1ull;
+          const uint32_t k = (uint32_t)LK(s);
+          if ((k >> 5) != bt) continue;
+          const uint32_t q = MS32(MF_PAD, s);
+          if (q < bq) { bq = q; bk = k; bs = s; }
+        }
+      }
+    }
+    x.mmin = bk == ~0u ? ~0ull : (((uint64_t)(bk >> 5) << 32) | (bk & 31u));
+    x.mslot = bs;
+    return;
+  }
   uint64_t best = ~0ull;
   uint32_t bs = 0;
   if constexpr (MR_RESCAN_OCC && MW == 1) {
@@ -386,6 +430,7 @@ DI int net_send(const Dev& D, X& x, uint32_t src, uint32_t& nctr, uint32_t dst, 
   }
   if (seq >= (1u << 25)) { fail(D, x, MR_FAIL_SIM_CAPACITY); return -1; }  // SEMANTICS §3, §9
   uint32_t t = x.now + u_range(w1, 1000u, net_lat_hi(x));
+  if (t >= T_KEY_MAX) { fail(D, x, MR_FAIL_SIM_CAPACITY); return -1; }  // SEMANTICS §4
   uint32_t slot = 0;
   if constexpr (MW == 1) {
     slot = (uint32_t)__builtin_ctzll(x.free_mask[0]);
@@ -403,14 +448,20 @@ DI int net_send(const Dev& D, X& x, uint32_t src, uint32_t& nctr, uint32_t dst, 
   }
   // key = (time, seq, dst): ordered as (time, seq) since seq is unique; dst (5
   // bits) in the low bits lets a delivery load the node's state before the message body
-  uint64_t key = ((uint64_t)t << 32) | (seq << 5) | dst;
-  LK(slot) = key;
   uint4* mp = reinterpret_cast<uint4*>(MSP(slot));
   mp[0] = make_uint4(hdr_make(type, src, dst, inc, k), term, a, b);
-  mp[1] = make_uint4(c, 0u, (uint32_t)v, (uint32_t)(v >> 32));
+  mp[1] = make_uint4(c, seq, (uint32_t)v, (uint32_t)(v >> 32));
   x.inflight++;
   CMAX(CNT_MAX_INFLIGHT, x.inflight);
-  if (key < x.mmin) { x.mmin = key; x.mslot = slot; }
+  if constexpr (MR_KEY32) {
+    LK(slot) = (t << 5) | dst;
+    // every message in flight has a smaller seq: a new one is earliest only by time
+    if (t < (uint32_t)(x.mmin >> 32)) { x.mmin = ((uint64_t)t << 32) | dst; x.mslot = slot; }
+  } else {
+    const uint64_t key = ((uint64_t)t << 32) | (seq << 5) | dst;
+    LK(slot) = key;
+    if (key < x.mmin) { x.mmin = key; x.mslot = slot; }
+  }
   return (int)slot;
 }
 
@@ -743,11 +794,13 @@ DI void node_event(const Dev& D, X& x, bool is_msg, uint32_t tnode, uint32_t slo
   if (is_msg) {
     const uint4 m0 = reinterpret_cast<const uint4*>(MSP(slot))[0];
     const uint32_t hdr = m0.x;
-    mterm = m0.y; ma = m0.z; mb = m0.w; mc = MS32(MF_C, slot);
+    const uint2 m1 = reinterpret_cast<const uint2*>(MSP(slot))[MF_C / 2];
+    mterm = m0.y; ma = m0.z; mb = m0.w; mc = m1.x;
+    if constexpr (MR_KEY32) seq = m1.y;  // the key carries no sequence number
     type = hdr_type(hdr); src = hdr_src(hdr); inc = hdr_inc(hdr);  // dst = tnode (key)
     k = hdr_k(hdr);
     hdr_bits = hdr;
-    LK(slot) = ~0ull;
+    LK(slot) = LKEY_FREE;
     if constexpr (MW == 1) {
       x.free_mask[0] |= 1ull << slot;
     } else {
@@ -1276,7 +1329,7 @@ __global__ void __launch_bounds__(STEP_BLOCK, MR_WAVES_PER_EU) step_kernel(Dev D
 #pragma unroll
     for (uint32_t k = 0; k < CNT__N; k++) x.cnt[k] = CS(CS_CNT + k);
 #endif
-    for (uint32_t s = 0; s < D.M; s++) LK(s) = MKEY(s);
+    for (uint32_t s = 0; s < D.M; s++) LK(s) = (lkey_t)MKEY(s);
   }
   const bool live = x.code == RUN;
   PROF(P_PRO);
@@ -1372,7 +1425,7 @@ __global__ void __launch_bounds__(STEP_BLOCK, MR_WAVES_PER_EU) step_kernel(Dev D
 #pragma unroll
   for (uint32_t k = 0; k < CNT__N; k++) CS(CS_CNT + k) = x.cnt[k];
 #endif
-  for (uint32_t s = 0; s < D.M; s++) MKEY(s) = LK(s);
+  for (uint32_t s = 0; s < D.M; s++) MKEY(s) = LK(s) == LKEY_FREE ? ~0ull : (uint64_t)LK(s);
   if (x.code == RUN) atomicAdd(D.remaining, 1u);
 }
 
@@ -1478,7 +1531,7 @@ hipError_t launch_reduce(const Dev& D, unsigned long long* out, uint64_t cluster
 template <uint32_t S, uint32_t NBT>
 hipError_t launch_step_t(const Dev& D, uint32_t budget, hipStream_t s) {
   dim3 blk(STEP_BLOCK), grd((D.C + STEP_BLOCK - 1) / STEP_BLOCK);
-  const size_t lds = (size_t)D.M * STEP_BLOCK * sizeof(uint64_t) +  // message keys
+  const size_t lds = (size_t)D.M * STEP_BLOCK * sizeof(lkey_t) +  // message keys
                     2 * MR_MAX_NODES * STEP_BLOCK * sizeof(uint32_t);  // send-loop staging
   hipLaunchKernelGGL((step_kernel<S, NBT>), grd, blk, lds, s, D, budget);
   return hipGetLastError();

@@ -322,6 +322,7 @@ static void net_send(OSim* s, uint32_t src, uint32_t dst, OMsg* m) {
   if (s->inflight >= s->cfg.msg_slots) { s->r.drop_overflow++; t_fail(s, MR_FAIL_SIM_CAPACITY); }
   if (seq >= (1u << 25)) t_fail(s, MR_FAIL_SIM_CAPACITY); /* SEMANTICS §3, §9 */
   m->time = s->now + u_range(w[1], s->lat_lo, s->lat_hi);
+  if (m->time >= (1u << 27) - 1u) t_fail(s, MR_FAIL_SIM_CAPACITY); /* SEMANTICS §4: t < 2^27 - 1 */
   m->seq = seq; m->src = (uint8_t)src; m->dst = (uint8_t)dst;
   uint32_t slot = s->free_stack[--s->n_free];
   s->pool[slot] = *m;

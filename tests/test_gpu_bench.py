@@ -93,3 +93,41 @@ def test_submit_finish_pipeline_equals_run(budget, monkeypatch):
         for x, y in zip(wv, gv):
             assert np.array_equal(x, y)
         assert wc == gc
+
+
+def _nccl_worker(port, q):
+    import torch
+    import torch.distributed as dist
+
+    from madraft_amd import dist as mdist
+    from madraft_amd import sim
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)  # RCCL
+    with sim.Batch("figure_8_unreliable_2c", 256, iters=50) as b:
+        b.run()
+        c = b.counters()
+    tot = mdist.allreduce_counters(c, device=dev)
+    t = mdist.allreduce_max(1.5, device=dev)
+    dist.destroy_process_group()
+    q.put(({k: tot[k] for k in ("events", "passed", "done", "max_inflight")},
+           {k: c[k] for k in ("events", "passed", "done", "max_inflight")}, t))
+
+
+def test_rccl_counter_allreduce_runs():
+    """The multi-GPU collective path (bench.py with --dist-backend nccl) executed on the GPU
+    box: RCCL all-reduce of a batch's counters on device tensors (world size 1 — one card),
+    equal to the counters themselves."""
+    import torch.multiprocessing as mp
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_nccl_worker, args=(port, q))
+    p.start()
+    tot, c, t = q.get(timeout=240)
+    p.join(timeout=60)
+    assert p.exitcode == 0
+    assert tot == c and t == 1.5 and c["done"] == 256
