@@ -86,7 +86,10 @@ struct X {
 // so a wave's 64 lanes read 64 consecutive u64 (conflict-free). Free slots hold
 // ~0, so the earliest-message scan is a branch-free min over all M slots.
 // lanes per block: 128, or 64 where 256 slots of keys must fit the 160 KiB of LDS
-constexpr uint32_t STEP_BLOCK = MW > 2 ? 64 : 128;
+#ifndef MR_BLOCK
+#define MR_BLOCK 128
+#endif
+constexpr uint32_t STEP_BLOCK = MW > 2 ? 64 : MR_BLOCK;
 // MR_KEY32: a 32-bit LDS key t << 5 | dst (t < 2^27 - 1, SEMANTICS §4); the (rare) tie of
 // two messages at the same t is broken by their sequence numbers, kept in the message
 // record (word MF_PAD). Otherwise a 64-bit key (t << 32 | seq << 5 | dst).
