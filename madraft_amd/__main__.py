@@ -1,10 +1,12 @@
 """CLI: `python -m madraft_amd <test> [--clusters N] [--seed S]` — the batched
-analogue of `MADSIM_TEST_SEED=S MADSIM_TEST_NUM=N cargo test <test>`."""
+analogue of `MADSIM_TEST_SEED=S MADSIM_TEST_NUM=N cargo test <test>`;
+`--replay log.jsonl` plays one cluster driven by an event-level decision log
+(madraft_amd/trace.py) and prints its verdict."""
 import argparse
 import json
 import time
 
-from . import _abi, sim
+from . import _abi, sim, trace
 
 
 def main():
@@ -20,11 +22,19 @@ def main():
                     help="per-event Raft invariant checks (docs/SEMANTICS.md §11)")
     ap.add_argument("--bug", choices=["vote_twice", "vote_stale", "no_prev_check"],
                     help="run a known-buggy Raft variant")
+    ap.add_argument("--replay", metavar="LOG", help="JSON-lines decision log (trace.py) to replay")
     a = ap.parse_args()
     flags = 0
     if a.bug:
         flags |= {"vote_twice": _abi.MR_F_BUG_VOTE_TWICE, "vote_stale": _abi.MR_F_BUG_VOTE_STALE,
                   "no_prev_check": _abi.MR_F_BUG_NO_PREV_CHECK}[a.bug]
+    if a.replay:
+        tr, code, tm, misses = sim.replay(a.test, trace.load_jsonl(a.replay), seed=a.seed or _abi.README_SEED,
+                                          nodes=a.nodes, iters=a.iters, unreliable=a.unreliable,
+                                          null_raft=a.null, safety=a.safety, flags=flags)
+        print(json.dumps({"code": code, "verdict": _abi.FAIL_NAMES.get(code, str(code)),
+                          "time_us": tm, "events": int(tr.size), "misses": misses}))
+        raise SystemExit(0 if code == _abi.MR_PASS else 1)
     t0 = time.time()
     code, _, _, cnt = sim.run_test(a.test, a.seed, a.clusters, nodes=a.nodes, iters=a.iters,
                                    unreliable=a.unreliable, null_raft=a.null, safety=a.safety,
