@@ -124,6 +124,8 @@ static inline uint32_t mr_kv_log_cap(uint32_t s) {
 /* Known-buggy kvraft servers (SEMANTICS §9): the linearizability checker must catch them */
 #define MR_F_BUG_NO_DEDUP 0x100u   /* servers re-apply a retried Put / Append (no per-clerk dedup) */
 #define MR_F_BUG_STALE_READ 0x200u /* a leader answers Get from its local state, not via the log */
+#define MR_F_STREAM 0x400u   /* with lanes < n_clusters: a lane whose cluster has its verdict takes
+                              * the next unstarted cluster (default: chunks of `lanes` clusters) */
 
 /* ---- verdicts: one code per tester panic site ---- */
 enum mr_fail {
@@ -213,7 +215,11 @@ typedef struct mr_cfg {
   uint32_t trace_cap;     /* trace records per traced cluster */
   int32_t device;         /* HIP device ordinal */
   uint32_t tape_cap;      /* with MR_F_RECORD: decisions kept per cluster */
-  uint32_t reserved[5];
+  uint32_t lanes;         /* clusters in flight per launch (0 = what the GPU keeps resident:
+                           * waves / SIMD x SIMDs x 64). A bigger batch runs as consecutive
+                           * chunks of `lanes` clusters (or streams them, MR_F_STREAM) instead of
+                           * queueing waves behind the resident ones. Results do not depend on it. */
+  uint32_t reserved[4];
 } mr_cfg;
 
 /* Whole-batch counters (sums over clusters unless named max/first). */

@@ -22,6 +22,7 @@ MR_F_BUG_NO_PREV_CHECK = 0x40
 MR_F_RECORD = 0x80
 MR_F_BUG_NO_DEDUP = 0x100
 MR_F_BUG_STALE_READ = 0x200
+MR_F_STREAM = 0x400  # lanes < clusters: finished lanes take the next cluster (mr_cfg.lanes)
 
 README_SEED = 1629626496  # /root/reference/README.md:48
 
@@ -83,7 +84,8 @@ class MrCfg(C.Structure):
         ("apply_cap", C.c_uint32), ("msg_slots", C.c_uint32), ("ae_max", C.c_uint32),
         ("hb_us", C.c_uint32), ("elect_lo_us", C.c_uint32), ("elect_hi_us", C.c_uint32),
         ("max_events", C.c_uint32), ("trace_clusters", C.c_uint32), ("trace_cap", C.c_uint32),
-        ("device", C.c_int32), ("tape_cap", C.c_uint32), ("reserved", C.c_uint32 * 5),
+        ("device", C.c_int32), ("tape_cap", C.c_uint32), ("lanes", C.c_uint32),
+        ("reserved", C.c_uint32 * 4),
     ]
 
 

@@ -46,13 +46,16 @@ def _units(csrc, scns=None):
         wide = [i for i in ids if i in WIDE_SLOTS]
         ids = [i for i in ids if i not in WIDE_SLOTS]
         ng = max(1, min(N_GROUPS, (len(ids) + 2) // 3)) if ids else 0
+        # 7- and 8-server runs keep up to 64 messages in flight: 32-bit LDS keys halve the
+        # key table so two waves per SIMD fit (config 4: +80 %)
+        key = ["-DMR_KEY32=1"] if nb == 8 else []
         for g in range(ng):
             lst = " ".join(f"MR_INST({i})" for i in ids[g::ng])
             units.append((kern, f"nb{nb}_{g}", ["-DMR_COMMON=0", f"-DMR_SCN_LIST={lst}",
-                                                f"-DMR_NB={nb}"]))
+                                                f"-DMR_NB={nb}", *key]))
         for i in wide:  # 256 message slots (mr_kernel.hip MR_MW)
             units.append((kern, f"nb{nb}_w{i}", ["-DMR_COMMON=0", f"-DMR_SCN_LIST=MR_INST({i})",
-                                                 f"-DMR_NB={nb}", "-DMR_MW=4"]))
+                                                 f"-DMR_NB={nb}", "-DMR_MW=4", *key]))
     ids = list(scns or SCN_IDS)  # decision-tape builds (SEMANTICS §12), NB = 8
     wide = [i for i in ids if i in WIDE_SLOTS]
     ids = [i for i in ids if i not in WIDE_SLOTS]

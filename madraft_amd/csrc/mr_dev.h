@@ -177,7 +177,10 @@ struct Dev {
   mr_event* trace;  // [trace_clusters][trace_cap]
   uint32_t* led;    // [C][LED_W] MR_F_SAFETY: bit t = a leader was elected in term t
   uint32_t* lin32;  // [C][KV_KEYS][KV_APP][LINW] kvraft linearizability bookkeeping (§9a)
-  uint32_t* remaining;  // clusters without verdict after a step launch
+  uint32_t* remaining;  // [2]: clusters without verdict after a step launch; next unclaimed cluster
+  uint32_t L;           // lanes per launch: lane l starts with cluster c0 + l (chunk [c0, c0 + L))
+  uint32_t c0;          // first cluster of this launch's chunk
+  uint32_t stream;      // MR_F_STREAM: a lane that finishes takes the next unclaimed cluster
   unsigned long long* prof;  // [PROF_SLOTS] wave-cycle profile (MR_PROF builds only)
 };
 constexpr uint32_t PROF_SLOTS = 64;
@@ -235,6 +238,9 @@ constexpr uint32_t nthr(uint32_t s) {
 // sized for its default server count (nb_of) and one for up to 8 servers
 template <uint32_t S, uint32_t NB>
 hipError_t launch_step_t(const Dev& D, uint32_t budget, hipStream_t s);
+// lanes the step kernel of scenario S keeps resident on the device (occupancy x CUs x block)
+template <uint32_t S, uint32_t NB>
+uint32_t step_capacity_t(int device, uint32_t M);
 // the same kernels built with decision-tape draws (MR_TAPE=1 translation units, NB = 8):
 // replay and record runs only, so the common draw path carries no tape branch
 template <uint32_t S, uint32_t NB>

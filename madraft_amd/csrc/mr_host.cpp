@@ -33,6 +33,22 @@ hipError_t launch_step(const Dev& D, uint32_t scn, uint32_t budget, hipStream_t 
     default: return hipErrorInvalidValue;
   }
 }
+// clusters the scenario's step kernel keeps resident (0: unknown)
+static uint32_t step_capacity(const Dev& D, uint32_t scn, int device) {
+  switch (scn) {
+#define MR_INST(S)                                                       \
+  case S:                                                                \
+    return D.n <= nb_of(S) ? step_capacity_t<S, nb_of(S)>(device, D.M)   \
+                           : step_capacity_t<S, MR_MAX_NODES>(device, D.M);
+#ifdef MR_DEV_SCNS
+    MR_DEV_SCNS
+#else
+    MR_ALL_SCNS
+#endif
+#undef MR_INST
+    default: return 0;
+  }
+}
 hipError_t launch_reset(const Dev& D, hipStream_t s);
 hipError_t launch_reduce(const Dev& D, unsigned long long* out, uint64_t cluster_base,
                          hipStream_t s);
@@ -83,7 +99,9 @@ struct mr_batch {
   void* base = nullptr;
   size_t bytes = 0;
   unsigned long long* red = nullptr;
-  uint32_t* h_remaining = nullptr;
+  uint32_t* h_remaining = nullptr;  // [2]: remaining, next unclaimed cluster (D.remaining)
+  uint32_t* h_ctl0 = nullptr;       // [2]: {0, L}, copied to D.remaining before each launch
+  uint32_t c_open = 0;              // first cluster of the first chunk not yet finished
   hipStream_t stream = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   uint32_t budget = 16384;  // events per cluster per launch (MR_STEP_BUDGET)
@@ -231,7 +249,10 @@ int mr_batch_create(const mr_cfg* cfg, mr_batch** out) {
   Dev& D = b->D;
   std::memset(&D, 0, sizeof D);
   const uint64_t C = cfg->n_clusters, n = cfg->n_nodes, M = cfg->msg_slots, K = cfg->ae_max;
-  D.C = (uint32_t)C; D.n = (uint32_t)n; D.log_cap = cfg->log_cap; D.apply_cap = cfg->apply_cap;
+  D.C = (uint32_t)C;
+  D.L = cfg->lanes && cfg->lanes < C ? cfg->lanes : (uint32_t)C;  // no tape: capacity (below)
+  D.stream = (cfg->flags & MR_F_STREAM) ? 1u : 0u;
+  D.n = (uint32_t)n; D.log_cap = cfg->log_cap; D.apply_cap = cfg->apply_cap;
   D.M = (uint32_t)M; D.K = (uint32_t)K; D.hb = cfg->hb_us; D.elo = cfg->elect_lo_us;
   D.ehi = cfg->elect_hi_us; D.max_events = cfg->max_events;
   D.null_raft = (cfg->flags & MR_F_NULL_RAFT) ? 1u : 0u;
@@ -289,7 +310,7 @@ int mr_batch_create(const mr_cfg* cfg, mr_batch** out) {
   }
   if (D.safety) add(&D.led, (size_t)LED_W * C);
   add(&D.trace, (size_t)D.trace_clusters * D.trace_cap);
-  add(&D.remaining, 1);
+  add(&D.remaining, 2);
   add(&D.prof, PROF_SLOTS);
   size_t total = 0;
   for (auto& it : items) total += (it.bytes + 255) & ~size_t(255);
@@ -297,7 +318,8 @@ int mr_batch_create(const mr_cfg* cfg, mr_batch** out) {
   hipError_t e = hipSetDevice(cfg->device);
   if (e == hipSuccess) e = hipMalloc(&b->base, total);
   if (e == hipSuccess) e = hipMalloc(&b->red, RED_N * sizeof(unsigned long long));
-  if (e == hipSuccess) e = hipHostMalloc(&b->h_remaining, sizeof(uint32_t));
+  if (e == hipSuccess) e = hipHostMalloc(&b->h_remaining, 2 * sizeof(uint32_t));
+  if (e == hipSuccess) e = hipHostMalloc(&b->h_ctl0, 2 * sizeof(uint32_t));
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&b->stream, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipEventCreate(&b->ev0);
   if (e == hipSuccess) e = hipEventCreate(&b->ev1);
@@ -327,6 +349,10 @@ int mr_batch_create(const mr_cfg* cfg, mr_batch** out) {
     mr_batch_destroy(b);
     return set_err("hipMemset failed");
   }
+  if (!cfg->lanes) {  // a batch bigger than the resident waves runs as chunks of that size
+    const uint32_t cap = step_capacity(b->D, scn, cfg->device);
+    if (cap && cap < b->D.C) b->D.L = cap;
+  }
   if (const char* s = std::getenv("MR_STEP_BUDGET")) b->budget = (uint32_t)std::atoi(s);
   if (b->budget == 0) b->budget = 16384;
   if (mr_batch_reset(b, cfg->seed_base) != 0) {
@@ -340,6 +366,7 @@ int mr_batch_create(const mr_cfg* cfg, mr_batch** out) {
 
 static int enqueue_reset(mr_batch* b, uint64_t seed_base) {
   b->cfg.seed_base = seed_base;
+  b->c_open = 0;
   b->D.seed0 = seed_base + b->cfg.cluster_base;
   HIPCHK(hipSetDevice(b->cfg.device));
   HIPCHK(hipMemsetAsync(b->D.stor, 0, (size_t)b->D.C * b->D.apply_cap * sizeof(SE), b->stream));
@@ -361,13 +388,23 @@ static int enqueue_reset(mr_batch* b, uint64_t seed_base) {
 // one step-kernel launch on the batch stream, bracketed by the timing events;
 // the remaining-cluster count is copied back asynchronously
 static int enqueue_step(mr_batch* b, uint32_t budget) {
-  HIPCHK(hipMemsetAsync(b->D.remaining, 0, sizeof(uint32_t), b->stream));
+  b->h_ctl0[0] = 0;
+  b->h_ctl0[1] = b->D.c0 + b->D.L;  // lanes start with clusters c0 .. c0+L-1 (streaming: claim on)
+  HIPCHK(hipMemcpyAsync(b->D.remaining, b->h_ctl0, 2 * sizeof(uint32_t), hipMemcpyHostToDevice,
+                        b->stream));
   HIPCHK(hipEventRecord(b->ev0, b->stream));
   HIPCHK(launch_step(b->D, b->D.scenario, budget, b->stream));
   HIPCHK(hipEventRecord(b->ev1, b->stream));
-  HIPCHK(hipMemcpyAsync(b->h_remaining, b->D.remaining, sizeof(uint32_t), hipMemcpyDeviceToHost,
+  HIPCHK(hipMemcpyAsync(b->h_remaining, b->D.remaining, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost,
                         b->stream));
   return 0;
+}
+
+// clusters of the launched chunk without a verdict: those the lanes held, plus (streaming)
+// those never claimed
+static uint64_t remaining_after(const mr_batch* b) {
+  const uint32_t next = b->h_remaining[1];
+  return (uint64_t)b->h_remaining[0] + (b->D.stream && next < b->D.C ? b->D.C - next : 0u);
 }
 
 int mr_batch_reset(mr_batch* b, uint64_t seed_base) {
@@ -386,28 +423,39 @@ int mr_batch_run(mr_batch* b, uint64_t max_events_per_call, mr_run_stats* st) {
   mr_run_stats s;
   std::memset(&s, 0, sizeof s);
   uint64_t done_events = 0;
-  for (;;) {
-    uint32_t budget = b->budget;
-    if (max_events_per_call) {
-      if (done_events >= max_events_per_call) break;
-      uint64_t left = max_events_per_call - done_events;
-      if (left < budget) budget = (uint32_t)left;
+  bool stop = false;
+  // chunks of D.L clusters, one after another (a streaming batch is one chunk of all clusters);
+  // a call cut short by max_events_per_call resumes with the chunk it stopped in
+  const uint32_t chunk = b->D.stream ? b->D.C : b->D.L;
+  for (uint32_t c0 = b->c_open; c0 < b->D.C && !stop; c0 += chunk) {
+    b->D.c0 = c0;
+    for (;;) {
+      uint32_t budget = b->budget;
+      if (max_events_per_call) {
+        if (done_events >= max_events_per_call) { stop = true; break; }
+        uint64_t left = max_events_per_call - done_events;
+        if (left < budget) budget = (uint32_t)left;
+      }
+      if (enqueue_step(b, budget) != 0) { b->D.c0 = 0; return -1; }
+      HIPCHK(hipStreamSynchronize(b->stream));
+      float ms = 0.f;
+      HIPCHK(hipEventElapsedTime(&ms, b->ev0, b->ev1));
+      s.kernel_ms += ms;
+      s.launches++;
+      done_events += budget;
+      if (remaining_after(b) == 0) {
+        b->c_open = c0 + chunk;
+        break;
+      }
     }
-    if (enqueue_step(b, budget) != 0) return -1;
-    HIPCHK(hipStreamSynchronize(b->stream));
-    float ms = 0.f;
-    HIPCHK(hipEventElapsedTime(&ms, b->ev0, b->ev1));
-    s.kernel_ms += ms;
-    s.launches++;
-    done_events += budget;
-    s.remaining = *b->h_remaining;
-    if (s.remaining == 0) break;
   }
+  b->D.c0 = 0;
   s.wall_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-  // events processed: sum of per-cluster event counters (cheap reduce)
+  // events processed and clusters left: sums over the per-cluster counters (cheap reduce)
   mr_counters c;
   if (mr_batch_counters(b, &c) != 0) return -1;
   s.events = c.events;
+  s.remaining = c.clusters - c.done;
   if (st) *st = s;
   return 0;
 }
@@ -437,7 +485,9 @@ int mr_batch_finish(mr_batch* b, mr_run_stats* st, mr_counters* cnt) {
   HIPCHK(hipEventElapsedTime(&ms, b->ev0, b->ev1));
   s.kernel_ms = ms;
   s.launches = 1;
-  s.remaining = *b->h_remaining;
+  s.remaining = remaining_after(b);
+  if (s.remaining == 0) b->c_open = b->D.stream ? b->D.C : b->D.L;  // the submitted chunk is done
+  if (b->c_open < b->D.C) s.remaining = 1;  // later chunks: run them below
   if (s.remaining != 0) {  // clusters past the per-launch budget: finish them synchronously
     mr_run_stats more;
     if (mr_batch_run(b, 0, &more) != 0) return -1;
@@ -654,6 +704,7 @@ void mr_batch_destroy(mr_batch* b) {
   if (b->tape) (void)hipFree(b->tape);
   if (b->red) (void)hipFree(b->red);
   if (b->h_remaining) (void)hipHostFree(b->h_remaining);
+  if (b->h_ctl0) (void)hipHostFree(b->h_ctl0);
   if (b->ev0) (void)hipEventDestroy(b->ev0);
   if (b->ev1) (void)hipEventDestroy(b->ev1);
   if (b->stream) (void)hipStreamDestroy(b->stream);

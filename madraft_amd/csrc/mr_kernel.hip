@@ -1304,6 +1304,75 @@ constexpr uint32_t CLS_MSG = 0, CLS_TIMER = 1, CLS_TESTER = 2, CLS_NONE = 3;
 #ifndef MR_WAVES_PER_EU
 #define MR_WAVES_PER_EU 2
 #endif
+// a cluster's run state into the lane (registers, LDS message keys) and back: at the start and
+// end of a launch, and when a lane that finished its cluster takes the next one (D.stream)
+template <uint32_t S>
+DI void lane_load(const Dev& D, X& x) {
+  x.code = CS(CS_CODE);
+  if (x.code != RUN) return;
+  x.now = CS(CS_NOW); x.events = CS(CS_EVENTS); x.msgs_sent = CS(CS_MSGS);
+  x.inflight = CS(CS_INFLIGHT); x.trace_n = CS(CS_TRACEN); x.mslot = CS(CS_MSLOT);
+  x.netmode = CS(CS_NETMODE); x.t_ctr = CS(CS_TCTR);
+  x.conn = CS(CS_CONN); x.alive = CS(CS_ALIVE); x.twake = CS(CS_TWAKE);
+  if constexpr (nthr(S) > 0) { x.cwake = CS(CS_CWAKE); x.ctid = CS(CS_CTID); x.cslot = CS(CS_CSLOT); }
+#pragma unroll
+  for (uint32_t d = 0; d < NB; d++) x.timer[d] = d < D.n ? TMR(d) : INF_T;
+#pragma unroll
+  for (uint32_t w = 0; w < MW; w++) x.free_mask[w] = C64(w ? C64_FREE1 + w - 1 : C64_FREE);
+  x.digest = C64(C64_DIGEST); x.mmin = C64(C64_MMIN);
+#if !MR_CNT_MEM
+#pragma unroll
+  for (uint32_t k = 0; k < CNT__N; k++) x.cnt[k] = CS(CS_CNT + k);
+#endif
+  for (uint32_t s = 0; s < D.M; s++) LK(s) = (lkey_t)MKEY(s);
+}
+template <uint32_t S>
+DI void lane_store(const Dev& D, X& x) {
+  CS(CS_CODE) = x.code;
+  if (x.code != RUN) CS(CS_VTIME) = x.now;
+  CS(CS_NOW) = x.now; CS(CS_EVENTS) = x.events; CS(CS_MSGS) = x.msgs_sent;
+  CS(CS_INFLIGHT) = x.inflight; CS(CS_TRACEN) = x.trace_n; CS(CS_MSLOT) = x.mslot;
+  CS(CS_NETMODE) = x.netmode; CS(CS_TCTR) = x.t_ctr;
+  CS(CS_CONN) = x.conn; CS(CS_ALIVE) = x.alive; CS(CS_TWAKE) = x.twake;
+  if constexpr (nthr(S) > 0) { CS(CS_CWAKE) = x.cwake; CS(CS_CTID) = x.ctid; CS(CS_CSLOT) = x.cslot; }
+#pragma unroll
+  for (uint32_t d = 0; d < NB; d++)
+    if (d < D.n) TMR(d) = x.timer[d];
+#pragma unroll
+  for (uint32_t w = 0; w < MW; w++) C64(w ? C64_FREE1 + w - 1 : C64_FREE) = x.free_mask[w];
+  C64(C64_DIGEST) = x.digest; C64(C64_MMIN) = x.mmin;
+#if !MR_CNT_MEM
+#pragma unroll
+  for (uint32_t k = 0; k < CNT__N; k++) CS(CS_CNT + k) = x.cnt[k];
+#endif
+  if (x.code != RUN) return;  // a finished cluster's messages are never read again
+  for (uint32_t s = 0; s < D.M; s++) MKEY(s) = LK(s) == LKEY_FREE ? ~0ull : (uint64_t)LK(s);
+}
+// lanes that want a cluster (`want`) take the next unclaimed ones, one atomic per wave per
+// round; a taken cluster that already has its verdict (a later launch of a long run) is
+// skipped. Returns whether this lane now holds a running cluster.
+template <uint32_t S>
+DI bool lane_claim(const Dev& D, X& x, bool want) {
+  bool held = false;
+  for (uint64_t wm = __ballot(want); wm; wm = __ballot(want)) {
+    const uint32_t first = (uint32_t)__builtin_ctzll(wm);
+    uint32_t base = 0;
+    if (__lane_id() == first) base = atomicAdd(&D.remaining[1], (uint32_t)__popcll(wm));
+    base = __shfl(base, (int)first);
+    if (want) {
+      x.c = base + (uint32_t)__popcll(wm & ((1ull << __lane_id()) - 1ull));
+      if (x.c >= D.C) {
+        want = false;
+        x.code = MR_PASS;  // nothing left: the lane idles
+      } else {
+        lane_load<S>(D, x);
+        if (x.code == RUN) { held = true; want = false; }
+      }
+    }
+  }
+  return held;
+}
+
 template <uint32_t S, uint32_t NBT>
 __global__ void __launch_bounds__(STEP_BLOCK, MR_WAVES_PER_EU) step_kernel(Dev D, uint32_t budget) {
   static_assert(NBT == NB, "one node bound per translation unit");
@@ -1315,26 +1384,12 @@ __global__ void __launch_bounds__(STEP_BLOCK, MR_WAVES_PER_EU) step_kernel(Dev D
     s_prof[threadIdx.x >> 6][2 * P__N] = wall_clock64();
   }
 #endif
-  const bool in = x.c < D.C;
-  x.code = in ? CS(CS_CODE) : (uint32_t)MR_PASS;
-  if (x.code == RUN) {
-    x.now = CS(CS_NOW); x.events = CS(CS_EVENTS); x.msgs_sent = CS(CS_MSGS);
-    x.inflight = CS(CS_INFLIGHT); x.trace_n = CS(CS_TRACEN); x.mslot = CS(CS_MSLOT);
-    x.netmode = CS(CS_NETMODE); x.t_ctr = CS(CS_TCTR);
-    x.conn = CS(CS_CONN); x.alive = CS(CS_ALIVE); x.twake = CS(CS_TWAKE);
-    if constexpr (nthr(S) > 0) { x.cwake = CS(CS_CWAKE); x.ctid = CS(CS_CTID); x.cslot = CS(CS_CSLOT); }
-#pragma unroll
-    for (uint32_t d = 0; d < NB; d++) x.timer[d] = d < D.n ? TMR(d) : INF_T;
-#pragma unroll
-    for (uint32_t w = 0; w < MW; w++) x.free_mask[w] = C64(w ? C64_FREE1 + w - 1 : C64_FREE);
-    x.digest = C64(C64_DIGEST); x.mmin = C64(C64_MMIN);
-#if !MR_CNT_MEM
-#pragma unroll
-    for (uint32_t k = 0; k < CNT__N; k++) x.cnt[k] = CS(CS_CNT + k);
-#endif
-    for (uint32_t s = 0; s < D.M; s++) LK(s) = (lkey_t)MKEY(s);
-  }
-  const bool live = x.code == RUN;
+  x.c += D.c0;  // lane l starts with cluster c0 + l of this launch's chunk
+  const bool in = x.c < D.c0 + D.L && x.c < D.C;
+  x.code = MR_PASS;
+  if (in) lane_load<S>(D, x);
+  bool held = x.code == RUN;  // this lane runs cluster x.c (its state is in registers / LDS)
+  if (D.stream) held = held || lane_claim<S>(D, x, in && !held);
   PROF(P_PRO);
   uint64_t key = 0;
   uint32_t cls = CLS_NONE, node = 0;
@@ -1342,6 +1397,14 @@ __global__ void __launch_bounds__(STEP_BLOCK, MR_WAVES_PER_EU) step_kernel(Dev D
   for (uint32_t it = 0; it < budget; it++) {
     asm volatile("" : "+v"(x.c));  // no LICM of per-lane addresses: recompute, do not keep live
     PROF(P_TAIL);
+    if (D.stream) {  // streaming lanes: the last iteration's finished clusters make way
+      const bool fin = held && x.code != RUN;
+      if (__ballot(fin)) {
+        if (fin) lane_store<S>(D, x);
+        const bool got = lane_claim<S>(D, x, fin);
+        if (fin) { held = got; need = true; }
+      }
+    }
     const bool run = x.code == RUN;
     if (__ballot(run) == 0) break;
     if (run && need) {  // next event: min over tester wake-up, node timers, earliest message
@@ -1410,25 +1473,8 @@ __global__ void __launch_bounds__(STEP_BLOCK, MR_WAVES_PER_EU) step_kernel(Dev D
       atomicAdd(&D.prof[32 + k], s_prof[threadIdx.x >> 6][P__N + k]);
     }
 #endif
-  if (!live) return;
-  CS(CS_CODE) = x.code;
-  if (x.code != RUN) CS(CS_VTIME) = x.now;
-  CS(CS_NOW) = x.now; CS(CS_EVENTS) = x.events; CS(CS_MSGS) = x.msgs_sent;
-  CS(CS_INFLIGHT) = x.inflight; CS(CS_TRACEN) = x.trace_n; CS(CS_MSLOT) = x.mslot;
-  CS(CS_NETMODE) = x.netmode; CS(CS_TCTR) = x.t_ctr;
-  CS(CS_CONN) = x.conn; CS(CS_ALIVE) = x.alive; CS(CS_TWAKE) = x.twake;
-  if constexpr (nthr(S) > 0) { CS(CS_CWAKE) = x.cwake; CS(CS_CTID) = x.ctid; CS(CS_CSLOT) = x.cslot; }
-#pragma unroll
-  for (uint32_t d = 0; d < NB; d++)
-    if (d < D.n) TMR(d) = x.timer[d];
-#pragma unroll
-  for (uint32_t w = 0; w < MW; w++) C64(w ? C64_FREE1 + w - 1 : C64_FREE) = x.free_mask[w];
-  C64(C64_DIGEST) = x.digest; C64(C64_MMIN) = x.mmin;
-#if !MR_CNT_MEM
-#pragma unroll
-  for (uint32_t k = 0; k < CNT__N; k++) CS(CS_CNT + k) = x.cnt[k];
-#endif
-  for (uint32_t s = 0; s < D.M; s++) MKEY(s) = LK(s) == LKEY_FREE ? ~0ull : (uint64_t)LK(s);
+  if (!held) return;
+  lane_store<S>(D, x);
   if (x.code == RUN) atomicAdd(D.remaining, 1u);
 }
 
@@ -1533,11 +1579,23 @@ hipError_t launch_reduce(const Dev& D, unsigned long long* out, uint64_t cluster
 
 template <uint32_t S, uint32_t NBT>
 hipError_t launch_step_t(const Dev& D, uint32_t budget, hipStream_t s) {
-  dim3 blk(STEP_BLOCK), grd((D.C + STEP_BLOCK - 1) / STEP_BLOCK);
+  dim3 blk(STEP_BLOCK), grd((D.L + STEP_BLOCK - 1) / STEP_BLOCK);
   const size_t lds = (size_t)D.M * STEP_BLOCK * sizeof(lkey_t) +  // message keys
                     2 * MR_MAX_NODES * STEP_BLOCK * sizeof(uint32_t);  // send-loop staging
   hipLaunchKernelGGL((step_kernel<S, NBT>), grd, blk, lds, s, D, budget);
   return hipGetLastError();
+}
+// clusters the step kernel keeps resident: blocks per CU (registers, LDS for M message slots)
+// x CUs x lanes per block
+template <uint32_t S, uint32_t NBT>
+uint32_t step_capacity_t(int device, uint32_t M) {
+  const size_t lds = (size_t)M * STEP_BLOCK * sizeof(lkey_t) + 2 * MR_MAX_NODES * STEP_BLOCK * sizeof(uint32_t);
+  int blocks = 0, cus = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, (const void*)step_kernel<S, NBT>, STEP_BLOCK,
+                                                   lds) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess)
+    return 0;
+  return (uint32_t)blocks * (uint32_t)cus * STEP_BLOCK;
 }
 // Step-kernel instances built by this translation unit: build.py compiles
 // this file once per scenario group (-DMR_SCN_LIST=...) in parallel, and once
@@ -1545,7 +1603,13 @@ hipError_t launch_step_t(const Dev& D, uint32_t budget, hipStream_t s) {
 #ifndef MR_SCN_LIST
 #define MR_SCN_LIST MR_ALL_SCNS
 #endif
+#if MR_TAPE  // replay / record batches run one launch of all their clusters
 #define MR_INST(S) template hipError_t launch_step_t<S, MR_NB>(const Dev&, uint32_t, hipStream_t);
+#else
+#define MR_INST(S)                                                                     \
+  template hipError_t launch_step_t<S, MR_NB>(const Dev&, uint32_t, hipStream_t);      \
+  template uint32_t step_capacity_t<S, MR_NB>(int, uint32_t);
+#endif
 MR_SCN_LIST
 #undef MR_INST
 

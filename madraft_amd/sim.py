@@ -77,7 +77,7 @@ def fail_message(code):
 
 def make_cfg(test, clusters=1, seed=_abi.README_SEED, *, nodes=None, iters=0, unreliable=False,
              null_raft=False, trace_clusters=0, trace_cap=None, cluster_base=0, device=0,
-             safety=False, **overrides):
+             safety=False, stream=False, **overrides):
     """mr_cfg for `test` with the reference's defaults (mr_cfg_init) plus overrides."""
     scn = _abi.SCENARIO_ID.get(test)
     if scn is None:
@@ -99,6 +99,8 @@ def make_cfg(test, clusters=1, seed=_abi.README_SEED, *, nodes=None, iters=0, un
         cfg.flags |= _abi.MR_F_NULL_RAFT
     if safety:
         cfg.flags |= _abi.MR_F_SAFETY
+    if stream:
+        cfg.flags |= _abi.MR_F_STREAM
     if trace_clusters:
         cfg.flags |= _abi.MR_F_TRACE
         cfg.trace_clusters = int(trace_clusters)

@@ -130,6 +130,26 @@ def test_step_budget_independence(hip):
         assert np.array_equal(a, c)
 
 
+@pytest.mark.parametrize("lanes,stream", [(1000, False), (1000, True), (64, True)])
+def test_lanes_chunks_and_streaming(hip, oracle, lanes, stream):
+    """Results do not depend on how many clusters are in flight: chunks of `lanes` clusters
+    one after another, or `lanes` streaming lanes that each take the next unstarted cluster
+    when theirs ends (mr_cfg.lanes, MR_F_STREAM) equal one lane per cluster and the oracle,
+    also when a launch's budget ends mid-way (max_events)."""
+    code, cnt = compare(hip, oracle, "figure_8_unreliable_2c", 2500, traced=3, iters=200,
+                        lanes=lanes, stream=stream)
+    with hip.Batch("figure_8_unreliable_2c", 2500, iters=200) as b:
+        b.run()
+        ref = b.verdicts()
+    with hip.Batch("figure_8_unreliable_2c", 2500, iters=200, lanes=lanes, stream=stream) as b:
+        while b.run(max_events=3001)["remaining"]:
+            pass
+        got = b.verdicts()
+        assert b.counters()["done"] == 2500
+    for a_, c_ in zip(ref, got):
+        assert np.array_equal(a_, c_)
+
+
 @pytest.mark.parametrize("test,clusters,kw", [
     ("fail_agree_2b", 65536, dict(nodes=5, unreliable=True)),     # BASELINE config 2
     ("figure_8_unreliable_2c", 131072, {}),                        # config 3, one GPU's shard
