@@ -31,6 +31,8 @@ N_GROUPS = 8
 WIDE_SLOTS = {42}
 
 
+# scenarios with a 7-server instance too (mr_dev.h has_nb7: the 2D tests, BASELINE config 4)
+NB7_SCNS = {19, 20, 21, 22, 23}
 # the scenarios' default server counts (mr_dev.h k_default_n): each scenario
 # gets an instance sized for it (NB = 3 or 5) and one for up to 8 servers
 DEFAULT_N = [0, 3, 3, 7, 5, 3, 5, 3, 3, 5, 3, 3, 5, 3, 5, 5, 5, 5, 5, 3, 3, 3, 3, 3, 5, 5, 5, 5, 3, 3, 5, 5, 5, 5, 5, 5, 5, 3, 5, 3, 3, 5, 5, 5, 5, 5]
@@ -39,8 +41,9 @@ DEFAULT_N = [0, 3, 3, 7, 5, 3, 5, 3, 3, 5, 3, 3, 5, 3, 5, 5, 5, 5, 5, 3, 3, 3, 3
 def _units(csrc, scns=None):
     kern = os.path.join(csrc, "mr_kernel.hip")
     units = [(kern, "common", ["-DMR_COMMON=1", "-DMR_SCN_LIST=", "-DMR_NB=8"])]
-    for nb in (3, 5, 8):
-        ids = [i for i in (scns or SCN_IDS) if nb == 8 or DEFAULT_N[i] == nb]
+    for nb in (3, 5, 7, 8):
+        ids = [i for i in (scns or SCN_IDS)
+               if nb == 8 or (DEFAULT_N[i] == nb if nb != 7 else i in NB7_SCNS)]
         if not ids:
             continue
         wide = [i for i in ids if i in WIDE_SLOTS]
@@ -48,7 +51,7 @@ def _units(csrc, scns=None):
         ng = max(1, min(N_GROUPS, (len(ids) + 2) // 3)) if ids else 0
         # 7- and 8-server runs keep up to 64 messages in flight: 32-bit LDS keys halve the
         # key table so two waves per SIMD fit (config 4: +80 %)
-        key = ["-DMR_KEY32=1"] if nb == 8 else []
+        key = ["-DMR_KEY32=1"] if nb >= 7 else []
         for g in range(ng):
             lst = " ".join(f"MR_INST({i})" for i in ids[g::ng])
             units.append((kern, f"nb{nb}_{g}", ["-DMR_COMMON=0", f"-DMR_SCN_LIST={lst}",

@@ -249,6 +249,11 @@ constexpr uint8_t k_default_n[] = {0, 3, 3, 7, 5, 3, 5, 3, 3, 5, 3, 3, 5, 3, 5,
                                    5, 5, 5, 5, 3, 3, 3, 3, 3, 5, 5, 5, 5, 3, 3,
                                    5, 5, 5, 5, 5, 5, 5, 3, 5, 3, 3, 5, 5, 5, 5, 5};
 constexpr uint32_t nb_of(uint32_t s) { return k_default_n[s] <= 5 ? k_default_n[s] : 8u; }
+// scenarios with a 7-server instance as well (BASELINE config 4 runs the 2D tests with 7
+// servers; arrays sized for 7 keep fewer registers live than the 8-server instance)
+constexpr bool has_nb7(uint32_t s) {
+  return s >= MR_SCN_SNAPSHOT_BASIC_2D && s <= MR_SCN_SNAPSHOT_INSTALL_UNRELIABLE_CRASH_2D;
+}
 #define MR_ALL_SCNS                                                                       \
   MR_INST(1) MR_INST(2) MR_INST(3) MR_INST(4) MR_INST(5) MR_INST(6) MR_INST(7) MR_INST(8) \
   MR_INST(9) MR_INST(10) MR_INST(11) MR_INST(12) MR_INST(13) MR_INST(14) MR_INST(16)      \

@@ -16,14 +16,17 @@
 #include "mr_dev.h"
 
 namespace mr {
+// the 7-server instance of S, where one is built (else the 8-server one: never reached)
+#define NB7_OF(S) (has_nb7(S) ? 7u : (uint32_t)MR_MAX_NODES)
 // the step-kernel instance of scenario `scn` (instances: MR_ALL_SCNS)
 hipError_t launch_step(const Dev& D, uint32_t scn, uint32_t budget, hipStream_t s) {
   switch (scn) {
 #define MR_INST(S)                                                                  \
   case S:                                                                           \
     return D.tape_mode ? launch_step_tape_t<S, MR_MAX_NODES>(D, budget, s)          \
-           : D.n <= nb_of(S) ? launch_step_t<S, nb_of(S)>(D, budget, s)             \
-                             : launch_step_t<S, MR_MAX_NODES>(D, budget, s);
+           : D.n <= nb_of(S)            ? launch_step_t<S, nb_of(S)>(D, budget, s)    \
+           : (has_nb7(S) && D.n == 7) ? launch_step_t<S, NB7_OF(S)>(D, budget, s)   \
+                                      : launch_step_t<S, MR_MAX_NODES>(D, budget, s);
 #ifdef MR_DEV_SCNS  // dev variants built for a few scenarios (build.py scns=)
     MR_DEV_SCNS
 #else
@@ -38,8 +41,9 @@ static uint32_t step_capacity(const Dev& D, uint32_t scn, int device) {
   switch (scn) {
 #define MR_INST(S)                                                       \
   case S:                                                                \
-    return D.n <= nb_of(S) ? step_capacity_t<S, nb_of(S)>(device, D.M)   \
-                           : step_capacity_t<S, MR_MAX_NODES>(device, D.M);
+    return D.n <= nb_of(S)            ? step_capacity_t<S, nb_of(S)>(device, D.M)   \
+           : (has_nb7(S) && D.n == 7) ? step_capacity_t<S, NB7_OF(S)>(device, D.M)   \
+                                      : step_capacity_t<S, MR_MAX_NODES>(device, D.M);
 #ifdef MR_DEV_SCNS
     MR_DEV_SCNS
 #else
