@@ -775,15 +775,29 @@ DI uint32_t on_ack(const Dev& D, X& x, uint32_t me, NC& d, uint32_t p, uint32_t 
 }
 
 // AC entries j.. of an AppendEntries payload (the sender's ring, or the
-// materialized copy) and the receiver's terms at their indices
+// materialized copy) and the receiver's entries at their indices: their terms, and (MR_F_SAFETY
+// log matching) their commands, from one 16-B load per entry
+#ifndef MR_AE_OWN
+#define MR_AE_OWN 1
+#endif
 DI void ae_load_batch(const Dev& D, const X& x, uint32_t me, const NC& d, uint32_t src, bool mat,
                       const LE* pp, uint32_t ma, uint32_t k, uint32_t j, LE (&pe)[AC],
-                      uint32_t (&lt)[AC]) {
+                      uint32_t (&lt)[AC], uint64_t (&ov)[AC]) {
 #pragma unroll
   for (uint32_t q = 0; q < AC; q++) {
     const uint32_t jx = j + q, i = ma + 1 + jx;
     pe[q] = jx < k ? (mat ? pp[jx] : D.log[logi(D, x, src, i)]) : LE{};
+#if MR_AE_OWN
+    // i > snap here (the caller skips a payload's prefix at or below the snapshot); the ring
+    // slot of any i is a valid address, so the safety checks' loads need no bound
+    const bool own = jx < k && (i <= d.last || D.safety);
+    const LE o = own ? D.log[logi(D, x, me, i)] : LE{};
+    lt[q] = (jx < k && i <= d.last) ? (i == d.last ? d.lastt : o.term) : 0u;
+    ov[q] = o.val;
+#else
     lt[q] = (jx < k && i <= d.last) ? term_at(D, x, me, d, i) : 0u;
+    ov[q] = 0;
+#endif
   }
 }
 
@@ -794,6 +808,22 @@ DI void node_event(const Dev& D, X& x, bool is_msg, uint32_t tnode, uint32_t slo
   uint32_t me = tnode, src = 0, type = 0, inc = 0, k = 0, mterm = 0, ma = 0, mb = 0, mc = 0;
   bool kvready = false;
   uint32_t hdr_bits = 0;
+#ifndef MR_NODE_FIRST  // the node record's loads issued before the message is decoded
+#define MR_NODE_FIRST 1
+#endif
+#if MR_NODE_FIRST
+  // the server is known from the event key, so its record, next[] / match[] and pending
+  // payload range are loaded together with the message (a clerk host has no record)
+  const bool has_rec = !KV || me < CLERK_HOST;
+  NC d = has_rec ? load_node(D, x, me) : NC{};
+  PV pv;
+  if (has_rec) load_peers(D, x, me, pv);
+#if MR_PLO_EARLY
+  const uint2 prange = has_rec ? reinterpret_cast<const uint2*>(NDP(me))[NF_PLO / 2] : make_uint2(0u, 0u);
+#else
+  const uint2 prange = make_uint2(0u, 0u);
+#endif
+#endif
   if (is_msg) {
     const uint4 m0 = reinterpret_cast<const uint4*>(MSP(slot))[0];
     const uint32_t hdr = m0.x;
@@ -821,6 +851,7 @@ DI void node_event(const Dev& D, X& x, bool is_msg, uint32_t tnode, uint32_t slo
       }
     }
   }
+#if !MR_NODE_FIRST
   NC d = load_node(D, x, me);
   PV pv;
   load_peers(D, x, me, pv);
@@ -828,6 +859,7 @@ DI void node_event(const Dev& D, X& x, bool is_msg, uint32_t tnode, uint32_t slo
   const uint2 prange = reinterpret_cast<const uint2*>(NDP(me))[NF_PLO / 2];
 #else
   const uint2 prange = make_uint2(0u, 0u);
+#endif
 #endif
   PROF(P_LOAD);
   uint32_t mode = SEND_NONE, peers = 0, rtype = 0, ra = 0, rb = 0, kind;
@@ -922,8 +954,9 @@ DI void node_event(const Dev& D, X& x, bool is_msg, uint32_t tnode, uint32_t slo
         // (sender's ring or materialized copy) and our terms at their indices
         LE pe[AC];
         uint32_t lt[AC];
+        uint64_t ov[AC];
         const uint32_t tp = term_at(D, x, me, d, prev);
-        ae_load_batch(D, x, me, d, src, mat, pp, ma, k, j0, pe, lt);
+        ae_load_batch(D, x, me, d, src, mat, pp, ma, k, j0, pe, lt, ov);
         PROF(P_AE_PROBE);
         if (!(D.bugs & MR_F_BUG_NO_PREV_CHECK) && tp != pterm) {
           uint32_t xx = prev;
@@ -933,11 +966,12 @@ DI void node_event(const Dev& D, X& x, bool is_msg, uint32_t tnode, uint32_t slo
         }
         CADD(CNT_SHIPPED, k - j0);  // the payload entries this receiver reads (zero-copy until here)
         for (uint32_t j = j0; j < k; j += AC) {
-          if (j != j0) ae_load_batch(D, x, me, d, src, mat, pp, ma, k, j, pe, lt);
+          if (j != j0) ae_load_batch(D, x, me, d, src, mat, pp, ma, k, j, pe, lt, ov);
           if (D.safety) {  // MR_F_SAFETY log matching: same index and term => same entry
-            uint64_t ov[AC];  // one batch of unconditional loads (ring addresses are always valid)
+#if !MR_AE_OWN
 #pragma unroll
             for (uint32_t q = 0; q < AC; q++) ov[q] = D.log[logi(D, x, me, ma + 1 + j + q)].val;
+#endif
             bool bad = false, skipping = true;  // skips form a prefix: the first write appends the rest
 #pragma unroll
             for (uint32_t q = 0; q < AC; q++) {
