@@ -524,13 +524,17 @@ DI void materialize(const Dev& D, X& x, uint32_t L, uint32_t& pexp) {
 }
 
 // before node L (pending deadline pexp) overwrites log index i
-DI void guard_log_write(const Dev& D, X& x, uint32_t L, uint32_t& pexp, uint32_t i) {
+DI void guard_log_write(const Dev& D, X& x, uint32_t L, uint32_t& pexp, uint32_t i, uint32_t plo,
+                        uint32_t phi) {  // plo / phi: L's pending payload range (NF_PLO, NF_PHI)
   if (x.now > pexp) return;  // every message L sent has been delivered
-  const uint32_t plo = ND(NF_PLO, L), phi = ND(NF_PHI, L);
   if (plo > phi) return;
   const uint32_t span = phi - plo;  // referenced j in [plo, phi] shares i's slot iff j = i mod cap
   if (span < D.log_cap - 1u && ((i - plo) & (D.log_cap - 1u)) > span) return;
   materialize(D, x, L, pexp);
+}
+DI void guard_log_write(const Dev& D, X& x, uint32_t L, uint32_t& pexp, uint32_t i) {
+  if (x.now > pexp) return;
+  guard_log_write(D, x, L, pexp, i, ND(NF_PLO, L), ND(NF_PHI, L));
 }
 
 // ---------------------------------------------------------------- tester storage
