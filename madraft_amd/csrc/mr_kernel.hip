@@ -182,10 +182,19 @@ __device__ __forceinline__ uint2 philox2(uint32_t c0, uint32_t c1, uint32_t c2, 
   c0 = (c0 ^ k0) * 0x9E3779B9u ^ (c1 + k1) * 0x85EBCA6Bu ^ c2 * 0xC2B2AE35u;
   return make_uint2(c0, c0 * 0x27D4EB2Fu + c2);
 #endif
+#ifndef MR_PHILOX_MAD64  // each round's two products as 64-bit v_mad_u64_u32 (A/B: DESIGN.md §6.6)
+#define MR_PHILOX_MAD64 1
+#endif
 #pragma unroll
   for (int r = 0; r < 10; r++) {
+#if MR_PHILOX_MAD64
+    const uint64_t p0 = (uint64_t)c0 * 0xD2511F53u, p1 = (uint64_t)c2 * 0xCD9E8D57u;
+    const uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
+    const uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
+#else
     uint32_t hi0 = __umulhi(0xD2511F53u, c0), lo0 = 0xD2511F53u * c0;
     uint32_t hi1 = __umulhi(0xCD9E8D57u, c2), lo1 = 0xCD9E8D57u * c2;
+#endif
     uint32_t n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
     c0 = n0; c1 = lo1; c2 = n2; c3 = lo0;
     k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
@@ -321,6 +330,27 @@ DI void rec_node(const Dev& D, X& x, uint32_t cls, uint32_t kind, uint32_t d, ui
   uint32_t role = bit(x.alive, d) ? f_role(n.f) : R_DOWN;
   rec8(D, x, x.now, cls | (kind << 8) | (d << 16) | (role << 24), aux, n.term, n.commit,
        n.applied, n.last, n.snap);
+}
+
+// a node event's trace record, taken as the event ends and appended by the step loop: one
+// copy of the record path (FNV digest, trace store) serves deliveries, drops and timer events,
+// so a wave whose lanes took different exits runs it once (MR_REC_ONCE)
+#ifndef MR_REC_ONCE
+#define MR_REC_ONCE 0
+#endif
+struct NR {
+  uint32_t w1, aux, term, commit, applied, last, snap;
+  bool on;
+};
+DI void nr_set(const Dev& D, X& x, NR& r, uint32_t cls, uint32_t kind, uint32_t d, uint32_t aux,
+               const NC& n) {
+#if MR_REC_ONCE
+  const uint32_t role = bit(x.alive, d) ? f_role(n.f) : R_DOWN;
+  r = NR{cls | (kind << 8) | (d << 16) | (role << 24), aux, n.term, n.commit, n.applied, n.last,
+         n.snap, true};
+#else
+  rec_node(D, x, cls, kind, d, aux, n);
+#endif
 }
 
 DI void rec_simple(const Dev& D, X& x, uint32_t cls, uint32_t kind) {
@@ -720,6 +750,136 @@ DI void node_apply(const Dev& D, X& x, uint32_t me, NC& d, bool& kvready) {
   d.slen = len;
 }
 
+// Cooperative applier (Raft-only scenarios; the KV services apply through a sequential state
+// machine and keep node_apply). The committed entries of every lane that reached the applier
+// in this wave iteration are spread over ALL those lanes, one entry per lane per round: a
+// lane with a backlog of hundreds of entries (a reconnected follower) costs the wave
+// ceil(total / lanes) round trips instead of one per batch of AC_APPLY of its own entries.
+// Exactly node_apply's result: the applier of tester.rs:302-325 with push_and_check
+// (tester.rs:366-396) is order-dependent only through the storage length `len` and the first
+// failure, both computed in closed form —
+//   * entries base..end (base = applied + 1, end = commit) have distinct indices, so their
+//     loads (log entry, checker record) and checks are independent;
+//   * the out-of-order failure can only hit the first entry (base > len); from index len on
+//     every entry is appended (len follows i), below it only checked;
+//   * the first failing entry f (lowest index, per cluster: an LDS atomic min over
+//     index << 2 | code) stops the cluster: entries below f are applied, f is counted unless
+//     it failed the capacity check (which precedes the count), nothing above f is written;
+//   * 2D service snapshots (every index with (i + 1) % 10 == 0 above the last) keep only the
+//     last: its term reaches the owner through LDS, its value goes straight to the record.
+// Helper work is found by a wave-uniform loop over the owning lanes (readlane), so lanes
+// that are not in this call never contribute a value.
+#ifndef MR_AP_COOP
+#define MR_AP_COOP 1
+#endif
+template <uint32_t S>
+DI void node_apply_coop(const Dev& D, X& x, uint32_t me, NC& d) {
+  constexpr bool SNAPS = has_nb7(S);  // snap_common (the 2D tests) runs with service snapshots
+  const bool snapmode = SNAPS && ((x.netmode >> 1) & 1u);
+  const uint32_t cnt = d.commit > d.applied ? d.commit - d.applied : 0u;
+  const uint32_t base = d.applied + 1u, len0 = d.slen;
+  // per-owner LDS words (the send-loop staging, unused until the send loop): first failure
+  // key, last snapshot's term
+  uint32_t* const fkw = reinterpret_cast<uint32_t*>(s_keys + D.M * STEP_BLOCK);
+  uint32_t* const stw = fkw + STEP_BLOCK;
+  const uint32_t lane = __lane_id(), wave0 = threadIdx.x - lane;
+  if (cnt) fkw[threadIdx.x] = ~0u;
+  const uint64_t act = __ballot(1);
+  const uint64_t own = __ballot(cnt != 0u);
+  const uint32_t nh = (uint32_t)__popcll(act);
+  const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(act >> 32),
+                                                 __builtin_amdgcn_mbcnt_lo((uint32_t)act, 0u));
+  uint32_t total = 0;
+  for (uint64_t m = own; m; m &= m - 1ull)
+    total += (uint32_t)__builtin_amdgcn_readlane((int)cnt, (int)__builtin_ctzll(m));
+  for (uint32_t w0 = 0; w0 < total; w0 += nh) {
+    // this lane's item w0 + rank: its owner lane o, index i, and o's cluster / node / length
+    const uint32_t w = w0 + rank;
+    uint32_t o = 64u, i = 0, oc = 0, ome = 0, olen = 0, obase = 0, oend = 0;
+    uint32_t pre = 0;
+    for (uint64_t m = own; m; m &= m - 1ull) {
+      const int ol = __builtin_ctzll(m);
+      const uint32_t oc_n = (uint32_t)__builtin_amdgcn_readlane((int)cnt, ol);
+      if (pre < w0 + nh && pre + oc_n > w0) {  // owner's range meets this round (uniform)
+        const uint32_t ob = (uint32_t)__builtin_amdgcn_readlane((int)base, ol);
+        if (w >= pre && w < pre + oc_n) {
+          o = (uint32_t)ol;
+          i = ob + (w - pre);
+          obase = ob;
+          oend = ob + oc_n - 1u;
+          oc = (uint32_t)__builtin_amdgcn_readlane((int)x.c, ol);
+          ome = (uint32_t)__builtin_amdgcn_readlane((int)me, ol);
+          olen = (uint32_t)__builtin_amdgcn_readlane((int)len0, ol);
+        }
+      }
+      pre += oc_n;
+      if (pre >= w0 + nh) break;
+    }
+    const bool mine = o < 64u;
+    // phase 1: loads and checks (node_apply's order: capacity, count, mismatch, out of order)
+    LE e = LE{};
+    SE s = SE{};
+    const bool inb = mine && i < D.apply_cap;
+    if (inb) {
+      e = D.log[((size_t)oc * D.n + ome) * D.log_cap + (i & (D.log_cap - 1u))];
+      s = D.stor[(size_t)oc * D.apply_cap + i];
+    }
+    if (mine) {
+      uint32_t key = ~0u;
+      if (!inb) key = (i << 2) | 0u;                                    // SIM_CAPACITY
+      else if (s.mask && s.val != e.val) key = (i << 2) | 1u;           // APPLY_MISMATCH
+      else if (i == obase && obase > olen) key = (i << 2) | 2u;         // APPLY_OUT_OF_ORDER
+      if (key != ~0u)
+        __hip_atomic_fetch_min(&fkw[wave0 + o], key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    // phase 2: entries below the owner's first failure are applied
+    if (mine) {
+      const uint32_t fk = fkw[wave0 + o];
+      const uint32_t f = fk == ~0u ? ~0u : fk >> 2;
+      if (i < f && i >= olen)  // i == len in node_apply's walk: appended
+        D.stor[(size_t)oc * D.apply_cap + i] = SE{e.val, s.mask | (1u << ome), e.term};
+      if (snapmode && i < f && (i + 1u) % 10u == 0u) {
+        // the last snapshot index of the applied range [obase, min(oend, f - 1)]
+        const uint32_t hi = f <= oend ? f - 1u : oend;
+        if (hi - i < 10u) {  // no later one in range: this entry is the snapshot kept
+          stw[wave0 + o] = e.term;
+          *reinterpret_cast<uint64_t*>(D.nd32 + ((size_t)oc * D.n + ome) * NREC + NF_SNAPV) = e.val;
+        }
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+  }
+  if (!cnt) return;
+  // the owner: counters and node state as node_apply leaves them
+  const uint32_t fk = fkw[threadIdx.x];
+  const uint32_t end = fk == ~0u ? d.commit : (fk >> 2) - 1u;  // last entry applied in full
+  const uint32_t napplied = end + 1u - base;                    // may be 0 (f == base)
+  CADD(CNT_APPLIES, napplied + (fk != ~0u && (fk & 3u) != 0u ? 1u : 0u));
+  if (end + 1u > len0 && napplied) {  // entries len0..end appended
+    CMAX(CNT_MAX_INDEX, end);
+    d.slen = end + 1u;
+  }
+  if (snapmode && napplied) {
+    const uint32_t lo = base > d.snap + 1u ? base : d.snap + 1u;
+    const uint32_t first = lo + (19u - lo % 10u) % 10u;  // smallest index >= lo with i % 10 == 9
+    if (first <= end) {
+      const uint32_t k = (end - first) / 10u + 1u;
+      d.snap = first + 10u * (k - 1u);
+      d.snapt = stw[threadIdx.x];
+      CADD(CNT_SNAPSHOTS, k);
+    }
+  }
+  d.applied = end;
+  if (fk != ~0u) {
+    const uint32_t code = fk & 3u;
+    fail(D, x, code == 0u ? MR_FAIL_SIM_CAPACITY : code == 1u ? MR_FAIL_APPLY_MISMATCH
+                                                              : MR_FAIL_APPLY_OUT_OF_ORDER);
+  }
+}
+
 // commit = the majority-th largest of the match indices mv[] (mv[me] = last),
 // if that entry is from the current term: for a leader, exactly the entries
 // above its base lbase (mr_dev.h NF record note), so no log access
@@ -807,7 +967,7 @@ DI void ae_load_batch(const Dev& D, const X& x, uint32_t me, const NC& d, uint32
 
 template <uint32_t S>
 DI void node_event(const Dev& D, X& x, bool is_msg, uint32_t tnode, uint32_t slot,
-                   uint32_t seq) {
+                   uint32_t seq, NR& nr) {
   constexpr bool KV = is_svc(S);  // kvraft / shard_ctrler request path
   uint32_t me = tnode, src = 0, type = 0, inc = 0, k = 0, mterm = 0, ma = 0, mb = 0, mc = 0;
   bool kvready = false;
@@ -866,20 +1026,33 @@ DI void node_event(const Dev& D, X& x, bool is_msg, uint32_t tnode, uint32_t slo
 #endif
 #endif
   PROF(P_LOAD);
+  // election-timer resets (raft.rs:260-263) are counted where the handlers call them and
+  // drawn once, after the handler: the timer keeps only the last draw, each draw is keyed by
+  // its own ectr (SEMANTICS §2), and nothing between reads the timer, so one Philox site
+  // serves every handler of the wave (MR_TAPE builds record every draw: immediate there)
+#ifndef MR_RESET_ONCE
+#define MR_RESET_ONCE 1
+#endif
+  uint32_t nrst = 0;
+#if MR_RESET_ONCE && !MR_TAPE
+#define RESET_ME() (nrst++)
+#else
+#define RESET_ME() reset_timer(D, x, me, d)
+#endif
   uint32_t mode = SEND_NONE, peers = 0, rtype = 0, ra = 0, rb = 0, kind;
   const uint32_t others = ((1u << D.n) - 1u) & ~(1u << me);
   if (is_msg) {
     kind = type;
     if (!bit(x.alive, me) || !bit(x.conn, me) || !bit(x.conn, src) || link_cut(D, x, src, me)) {
       CADD(CNT_DROP_DELIVER, 1u);
-      rec_node(D, x, 0, 16, me, seq, d);
+      nr_set(D, x, nr, 0, 16, me, seq, d);
       PROF(P_DROP);
       return;
     }
     bool is_reply = (type == M_RV_REP || type == M_AE_REP || type == M_IS_REP);
     if (is_reply && inc != f_inc(d.f)) {
       CADD(CNT_DROP_STALE, 1u);
-      rec_node(D, x, 0, 17, me, seq, d);
+      nr_set(D, x, nr, 0, 17, me, seq, d);
       PROF(P_DROP);
       return;
     }
@@ -888,7 +1061,7 @@ DI void node_event(const Dev& D, X& x, bool is_msg, uint32_t tnode, uint32_t slo
         kv_request(D, x, me, d, src, inc, mterm, ma, mb, mc);
         if (x.code != RUN) return;
         store_node(D, x, me, d);
-        rec_node(D, x, 0, type, me, seq, d);
+        nr_set(D, x, nr, 0, type, me, seq, d);
         return;
       }
     }
@@ -896,7 +1069,7 @@ DI void node_event(const Dev& D, X& x, bool is_msg, uint32_t tnode, uint32_t slo
       uint32_t was = f_role(d.f);
       d.term = mterm;
       d.f = f_set(f_set(f_set(d.f, 4, 4, 15u), 16, 8, 0u), 0, 2, R_F);
-      if (was == R_L) reset_timer(D, x, me, d);
+      if (was == R_L) RESET_ME();
       PROF(P_STEPDOWN);
     }
     const uint32_t role = f_role(d.f), term = d.term;
@@ -910,7 +1083,7 @@ DI void node_event(const Dev& D, X& x, bool is_msg, uint32_t tnode, uint32_t slo
         bool granted = (mterm == term) && free_vote && up;
         if (granted) {
           d.f = f_set(d.f, 4, 4, ma);
-          reset_timer(D, x, me, d);
+          RESET_ME();
         }
         mode = SEND_REPLY; rtype = M_RV_REP; ra = granted ? 1u : 0u;
         PROF(P_RVREQ);
@@ -944,7 +1117,7 @@ DI void node_event(const Dev& D, X& x, bool is_msg, uint32_t tnode, uint32_t slo
         mode = SEND_REPLY; rtype = M_AE_REP;
         if (mterm < term) break;  // reply {term, false, 0}
         if (role == R_C) d.f = f_set(d.f, 0, 2, R_F);
-        reset_timer(D, x, me, d);
+        RESET_ME();
         uint32_t prev = ma, pterm = mb, j0 = 0;
         if (prev < d.snap) {
           uint32_t skip = d.snap - prev;
@@ -1025,7 +1198,7 @@ DI void node_event(const Dev& D, X& x, bool is_msg, uint32_t tnode, uint32_t slo
         mode = SEND_REPLY; rtype = M_IS_REP;
         if (mterm < term) break;  // reply {term, 0}
         if (role == R_C) d.f = f_set(d.f, 0, 2, R_F);
-        reset_timer(D, x, me, d);
+        RESET_ME();
         uint32_t idx = ma;
         if (idx > d.commit) {
           if (!(idx <= d.last && term_at(D, x, me, d, idx) == mb)) { d.last = idx; d.lastt = mb; }
@@ -1060,10 +1233,15 @@ DI void node_event(const Dev& D, X& x, bool is_msg, uint32_t tnode, uint32_t slo
     d.term++;
     d.f = f_set(f_set(f_set(d.f, 4, 4, me), 0, 2, R_C), 16, 8, 1u << me);
     CADD(CNT_ELECTIONS, 1u);
-    reset_timer(D, x, me, d);
+    RESET_ME();
     mode = SEND_VOTE; peers = others;
     PROF(P_ELECT);
   }
+  if (nrst) {  // the last of this event's nrst draws (ectr advances by nrst, as drawn inline)
+    d.ectr += nrst - 1u;
+    reset_timer(D, x, me, d);
+  }
+#undef RESET_ME
   // peers a send can reach: one from a disconnected sender or to a disconnected destination
   // clogs (net_send, SEMANTICS §4), so it needs only its accounting — a sequence number, a
   // send index, drop_clog — and none of the send path's loads (MR_TAPE builds record its
@@ -1082,7 +1260,13 @@ DI void node_event(const Dev& D, X& x, bool is_msg, uint32_t tnode, uint32_t slo
     rawt[p] = (mode == SEND_APPEND && bit(peers & reach, p) && p < D.n && ix != 0u) ? D.log[logi(D, x, me, ix)].term : 0u;
   }
 #endif
-  if (d.applied < d.commit) {  // committed entries reach the tester's applier
+  if (MR_AP_COOP && !KV && kv_gen(S).maxraft == 0) {
+    if (__ballot(d.applied < d.commit)) {  // committed entries reach the tester's applier
+      node_apply_coop<S>(D, x, me, d);
+      if (x.code != RUN) return;
+      PROF(P_APPLY);
+    }
+  } else if (d.applied < d.commit) {
     node_apply<S>(D, x, me, d, kvready);
     if (x.code != RUN) return;
     PROF(P_APPLY);
@@ -1165,7 +1349,7 @@ DI void node_event(const Dev& D, X& x, bool is_msg, uint32_t tnode, uint32_t slo
   }
   PROF(P_SEND);
   store_node(D, x, me, d);
-  rec_node(D, x, is_msg ? 0u : 1u, kind, me, is_msg ? seq : 0u, d);
+  nr_set(D, x, nr, is_msg ? 0u : 1u, kind, me, is_msg ? seq : 0u, d);
   PROF(P_STORE);
 }
 
@@ -1496,7 +1680,11 @@ __global__ void __launch_bounds__(STEP_BLOCK, step_waves<S>()) step_kernel(Dev D
     if (x.events > D.max_events) { fail(D, x, MR_FAIL_SIM_EVENT_LIMIT); continue; }
     if (cls != CLS_TESTER) {
       CADD(cls == CLS_MSG ? CNT_EV_MSG : CNT_EV_TIMER, 1u);
-      node_event<S>(D, x, cls == CLS_MSG, node, x.mslot, ((uint32_t)key & 0x3FFFFFFFu) >> 5);
+      NR nr;
+      nr.on = false;
+      node_event<S>(D, x, cls == CLS_MSG, node, x.mslot, ((uint32_t)key & 0x3FFFFFFFu) >> 5, nr);
+      if (MR_REC_ONCE && nr.on && x.code == RUN)
+        rec8(D, x, x.now, nr.w1, nr.aux, nr.term, nr.commit, nr.applied, nr.last, nr.snap);
     } else {
       CADD(CNT_EV_TESTER, 1u);
       if constexpr (nthr(S) > 0) {

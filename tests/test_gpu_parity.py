@@ -190,6 +190,24 @@ def test_safety_checks_bit_exact(hip, oracle, test, flags):
         assert not np.isin(code, [42, 43, 49]).any()
 
 
+@pytest.mark.parametrize("test,kw", [
+    ("figure_8_unreliable_2c", dict(flags=_abi.MR_F_BUG_VOTE_STALE)),
+    ("figure_8_unreliable_2c", dict(flags=_abi.MR_F_BUG_NO_PREV_CHECK)),
+    ("snapshot_install_unreliable_2d", dict(flags=_abi.MR_F_BUG_VOTE_STALE)),
+    ("snapshot_install_unreliable_2d", dict(flags=_abi.MR_F_BUG_VOTE_TWICE, nodes=7)),
+    ("figure_8_unreliable_2c", dict(apply_cap=64)),
+    ("snapshot_basic_2d", dict(apply_cap=40)),
+])
+def test_apply_checker_failures_bit_exact(hip, oracle, test, kw):
+    """The tester's apply checker (push_and_check, tester.rs:366-396) failing inside the
+    cooperative applier (entries of one cluster spread over the wave's lanes): buggy Rafts
+    without MR_F_SAFETY commit diverging entries (APPLY_MISMATCH), a tiny apply_cap trips
+    the capacity check; verdict, time, trace digest, traced records and counters (applies,
+    snapshots, max_index) equal the oracle's sequential walk."""
+    code, _ = compare(hip, oracle, test, 256, **kw)
+    assert np.isin(code, [8, 9, 60]).sum() >= 20
+
+
 @pytest.mark.parametrize("test,flags", [
     ("unreliable_3a", _abi.MR_F_BUG_NO_DEDUP),
     ("unreliable_one_key_3a", _abi.MR_F_BUG_NO_DEDUP),
