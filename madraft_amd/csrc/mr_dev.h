@@ -55,6 +55,8 @@ enum : uint32_t {
   CS_TAPE,   // keyed decisions: recorded so far (record) / draws without a record (replay)
   CS_KV_OPS, CS_KV_CHECKED,  // service clerk calls completed / Get results verified
   CS_KV_LIN,                 // Get results the linearizability checker verified
+  CS_LRS,                    // per node: run start of its last log entry (mr_kernel.hip rs_of)
+  CS_LRS_END = CS_LRS + 8,
   CS__N
 };
 // cs64 [C64__N][C]: per-cluster u64 scalars
@@ -81,8 +83,8 @@ enum : uint32_t { MF_HDR, MF_TERM, MF_A, MF_B, MF_C, MF_PAD, MF_V, MREC = 8 };
 // one Raft log entry (raft.rs Log: term + command), 16 B so an entry moves as
 // one 128-bit access; message payloads (AppendEntries entries) use the same form
 struct alignas(16) LE {
-  uint32_t term, pad;
-  uint64_t val;
+  uint32_t term, rs;  // rs: first index of the run of entries of this term that ends here
+  uint64_t val;       // (device log only; <= the snapshot index when the run reaches it)
 };
 
 // ---- kvraft (SEMANTICS §8-9); arrays allocated for the kvraft scenarios only

@@ -293,6 +293,28 @@ DI uint32_t term_at(const Dev& D, const X& x, uint32_t d, const NC& n, uint32_t 
   return D.log[logi(D, x, d, i)].term;
 }
 
+// Run starts (fast backup in O(1)): every log entry written on the device carries rs = the
+// first index of the run of equal terms that ends at it (LE.rs), computed from the entry
+// below it as it is written — rs(i) = rs(i - 1) if term(i) == term(i - 1), else i — and
+// CS_LRS + d keeps rs(last) so an append needs no log read. Below or at the snapshot the
+// entries are gone: the entry at the snapshot index counts with rs = snap, so a stored rs is
+// either the run's true start or <= snap, and the fast-backup walk of a conflicting term
+// (raft.rs AppendEntries handler; the oracle walks entry by entry)
+//   xx = prev; while (xx - 1 > snap && term(xx - 1) == term(prev)) xx--;
+// is xx = max(rs(prev), snap + 1) for prev > snap — one load instead of one round trip per
+// entry of the run (figure_8_unreliable: 16-127 entries per walk, ≈ 40 walks per seed).
+// (term, rs) of entry i of node d: the snapshot, cached last entry, or the ring
+DI void le_at(const Dev& D, const X& x, uint32_t d, const NC& n, uint32_t lrs, uint32_t i,
+              uint32_t& t, uint32_t& rs) {
+  if (i == 0) { t = 0; rs = 0; return; }
+  if (i == n.snap) { t = n.snapt; rs = n.snap; return; }
+  if (i == n.last) { t = n.lastt; rs = lrs; return; }
+  const LE e = D.log[logi(D, x, d, i)];
+  t = e.term;
+  rs = e.rs;
+}
+#define LRS(d) CS(CS_LRS + (d))
+
 // message header word: type[0:4) src[4:9) dst[9:14) inc/tag[14:22) k[22:28) MAT[28]
 // (hosts: servers 0..7, clerks 8..31)
 DI uint32_t hdr_make(uint32_t type, uint32_t src, uint32_t dst, uint32_t inc, uint32_t k) {
@@ -946,7 +968,7 @@ DI uint32_t on_ack(const Dev& D, X& x, uint32_t me, NC& d, uint32_t p, uint32_t 
 #endif
 DI void ae_load_batch(const Dev& D, const X& x, uint32_t me, const NC& d, uint32_t src, bool mat,
                       const LE* pp, uint32_t ma, uint32_t k, uint32_t j, LE (&pe)[AC],
-                      uint32_t (&lt)[AC], uint64_t (&ov)[AC]) {
+                      uint32_t (&lt)[AC], uint64_t (&ov)[AC], uint32_t (&ors)[AC]) {
 #pragma unroll
   for (uint32_t q = 0; q < AC; q++) {
     const uint32_t jx = j + q, i = ma + 1 + jx;
@@ -958,9 +980,11 @@ DI void ae_load_batch(const Dev& D, const X& x, uint32_t me, const NC& d, uint32
     const LE o = own ? D.log[logi(D, x, me, i)] : LE{};
     lt[q] = (jx < k && i <= d.last) ? (i == d.last ? d.lastt : o.term) : 0u;
     ov[q] = o.val;
+    ors[q] = o.rs;
 #else
     lt[q] = (jx < k && i <= d.last) ? term_at(D, x, me, d, i) : 0u;
     ov[q] = 0;
+    ors[q] = (jx < k && i < d.last && i > d.snap) ? D.log[logi(D, x, me, i)].rs : 0u;
 #endif
   }
 }
@@ -1130,20 +1154,31 @@ DI void node_event(const Dev& D, X& x, bool is_msg, uint32_t tnode, uint32_t slo
         // one batch of independent loads: prev's term, then AC payload entries
         // (sender's ring or materialized copy) and our terms at their indices
         LE pe[AC];
-        uint32_t lt[AC];
+        uint32_t lt[AC], ors[AC];
         uint64_t ov[AC];
-        const uint32_t tp = term_at(D, x, me, d, prev);
-        ae_load_batch(D, x, me, d, src, mat, pp, ma, k, j0, pe, lt, ov);
+        const uint32_t lrs = LRS(me);
+        uint32_t tp, rsp;  // term and run start of our entry at prev
+        le_at(D, x, me, d, lrs, prev, tp, rsp);
+        ae_load_batch(D, x, me, d, src, mat, pp, ma, k, j0, pe, lt, ov, ors);
         PROF(P_AE_PROBE);
         if (!(D.bugs & MR_F_BUG_NO_PREV_CHECK) && tp != pterm) {
+#ifndef MR_RUNSTART
+#define MR_RUNSTART 1
+#endif
+#if MR_RUNSTART  // fast backup: the run of term tp holding prev starts at rs(prev) (le_at)
+          rb = prev <= d.snap ? prev : (rsp > d.snap + 1u ? rsp : d.snap + 1u);
+#else
           uint32_t xx = prev;
           while (xx - 1 > d.snap && term_at(D, x, me, d, xx - 1) == tp) xx--;
           rb = xx;
+#endif
           break;
         }
+        uint32_t tprev = tp, rsprev = rsp;  // the entry below the next one written
+        bool wrote = false;
         CADD(CNT_SHIPPED, k - j0);  // the payload entries this receiver reads (zero-copy until here)
         for (uint32_t j = j0; j < k; j += AC) {
-          if (j != j0) ae_load_batch(D, x, me, d, src, mat, pp, ma, k, j, pe, lt, ov);
+          if (j != j0) ae_load_batch(D, x, me, d, src, mat, pp, ma, k, j, pe, lt, ov, ors);
           if (D.safety) {  // MR_F_SAFETY log matching: same index and term => same entry
 #if !MR_AE_OWN
 #pragma unroll
@@ -1163,16 +1198,24 @@ DI void node_event(const Dev& D, X& x, bool is_msg, uint32_t tnode, uint32_t slo
           for (uint32_t q = 0; q < AC; q++) {
             const uint32_t jx = j + q, i = ma + 1 + jx;
             if (jx >= k) break;
-            if (i <= d.last && lt[q] == pe[q].term) continue;  // d.last only drops below i here
+            if (i <= d.last && lt[q] == pe[q].term) {  // d.last only drops below i here
+              tprev = lt[q];
+              rsprev = i == d.last ? lrs : ors[q];
+              continue;
+            }
             if (i - d.snap > D.log_cap) { fail(D, x, MR_FAIL_SIM_CAPACITY); return; }
             guard_log_write(D, x, me, d.pexp, i);
-            D.log[logi(D, x, me, i)] = pe[q];
+            rsprev = pe[q].term == tprev ? rsprev : i;
+            tprev = pe[q].term;
+            D.log[logi(D, x, me, i)] = LE{pe[q].term, rsprev, pe[q].val};
+            wrote = true;
             CADD(CNT_LOG_WRITES, 1u);
             d.last = i;
             d.lastt = pe[q].term;
             CMAX(CNT_MAX_LOG, i - d.snap);
           }
         }
+        if (wrote) LRS(me) = rsprev;
         uint32_t lc = ma + k;
         if (mc < lc) lc = mc;
         if (lc > d.commit) d.commit = lc;
@@ -1201,7 +1244,10 @@ DI void node_event(const Dev& D, X& x, bool is_msg, uint32_t tnode, uint32_t slo
         RESET_ME();
         uint32_t idx = ma;
         if (idx > d.commit) {
-          if (!(idx <= d.last && term_at(D, x, me, d, idx) == mb)) { d.last = idx; d.lastt = mb; }
+          if (!(idx <= d.last && term_at(D, x, me, d, idx) == mb)) {
+            d.last = idx; d.lastt = mb;
+            LRS(me) = idx;  // the snapshot entry (rs <= snap)
+          }
           d.snap = idx; d.snapt = mb; NSV(me) = MSV(slot);
           d.commit = idx; d.applied = idx;
           storage_snapshot(D, x, me, d.slen, idx);
@@ -1404,9 +1450,11 @@ DI bool t_start(const Dev& D, X& x, uint32_t i, uint64_t v, uint32_t& idx, uint3
   size_t li = logi(D, x, i, last);
   term = ND(NF_TERM, i);
   uint32_t pexp = ND(NF_PEXP, i);
+  const uint32_t rs = term == ND(NF_LASTT, i) ? LRS(i) : last;  // run start (le_at)
   guard_log_write(D, x, i, pexp, last);
   ND(NF_PEXP, i) = pexp;
-  D.log[li] = LE{term, 0u, v};
+  D.log[li] = LE{term, rs, v};
+  LRS(i) = rs;
   CADD(CNT_LOG_WRITES, 1u);
   ND(NF_LAST, i) = last;
   ND(NF_LASTT, i) = term;
