@@ -55,7 +55,8 @@ enum : uint32_t {
   CS_TAPE,   // keyed decisions: recorded so far (record) / draws without a record (replay)
   CS_KV_OPS, CS_KV_CHECKED,  // service clerk calls completed / Get results verified
   CS_KV_LIN,                 // Get results the linearizability checker verified
-  CS_LRS,                    // per node: run start of its last log entry (mr_kernel.hip rs_of)
+  CS_LMASK,                  // servers whose record holds role leader (x.lmask, store_node)
+  CS_LRS,                    // per node: run start of its last log entry (mr_kernel.hip le_at)
   CS_LRS_END = CS_LRS + 8,
   CS__N
 };

@@ -63,6 +63,7 @@ struct X {
   uint32_t sleep_us, yield, twake;  // twake: the tester's next wake-up (CS_TWAKE)
   uint32_t cwake, ctid, cslot;      // kvraft: earliest client thread (wake, tid, slot)
   uint32_t conn, alive;  // node bit masks: connected (net clog state), started (tester.rs:24-25)
+  uint32_t lmask;        // servers whose stored role is leader (kept by store_node)
   uint64_t free_mask[MW], digest, mmin;
   uint32_t timer[NB];  // node timers (election / heartbeat deadline), INF_T = none
 #if !MR_CNT_MEM
@@ -252,7 +253,10 @@ DI NC load_node(const Dev& D, const X& x, uint32_t d) {
   const uint4 a = p[0], b = p[1], c = p[2];
   return NC{a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w, c.x, c.y, c.z, c.w};
 }
-DI void store_node(const Dev& D, const X& x, uint32_t d, const NC& n) {
+// every role change of a record passes here, so x.lmask mirrors the stored roles and the
+// tester's is_leader() sampling (t_leaders) reads no record
+DI void store_node(const Dev& D, X& x, uint32_t d, const NC& n) {
+  x.lmask = (x.lmask & ~(1u << d)) | (f_role(n.f) == R_L ? 1u << d : 0u);
   uint4* p = reinterpret_cast<uint4*>(NDP(d));
   p[0] = make_uint4(n.f, n.term, n.commit, n.applied);
   p[1] = make_uint4(n.last, n.snap, n.snapt, n.ectr);
@@ -796,8 +800,9 @@ DI void node_apply(const Dev& D, X& x, uint32_t me, NC& d, bool& kvready) {
 #endif
 template <uint32_t S>
 DI void node_apply_coop(const Dev& D, X& x, uint32_t me, NC& d) {
-  constexpr bool SNAPS = has_nb7(S);  // snap_common (the 2D tests) runs with service snapshots
-  const bool snapmode = SNAPS && ((x.netmode >> 1) & 1u);
+  // snap_common (the 2D tests, has_nb7) runs with service snapshots: t_new(snapshot = true)
+  // precedes every node event of such a batch, so the mode is the same for every lane here
+  constexpr bool snapmode = has_nb7(S);
   const uint32_t cnt = d.commit > d.applied ? d.commit - d.applied : 0u;
   const uint32_t base = d.applied + 1u, len0 = d.slen;
   // per-owner LDS words (the send-loop staging, unused until the send loop): first failure
@@ -812,6 +817,7 @@ DI void node_apply_coop(const Dev& D, X& x, uint32_t me, NC& d) {
   const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(act >> 32),
                                                  __builtin_amdgcn_mbcnt_lo((uint32_t)act, 0u));
   uint32_t total = 0;
+  bool anyfail = false;
   for (uint64_t m = own; m; m &= m - 1ull)
     total += (uint32_t)__builtin_amdgcn_readlane((int)cnt, (int)__builtin_ctzll(m));
   for (uint32_t w0 = 0; w0 < total; w0 += nh) {
@@ -846,19 +852,23 @@ DI void node_apply_coop(const Dev& D, X& x, uint32_t me, NC& d) {
       e = D.log[((size_t)oc * D.n + ome) * D.log_cap + (i & (D.log_cap - 1u))];
       s = D.stor[(size_t)oc * D.apply_cap + i];
     }
+    uint32_t key = ~0u;
     if (mine) {
-      uint32_t key = ~0u;
       if (!inb) key = (i << 2) | 0u;                                    // SIM_CAPACITY
       else if (s.mask && s.val != e.val) key = (i << 2) | 1u;           // APPLY_MISMATCH
       else if (i == obase && obase > olen) key = (i << 2) | 2u;         // APPLY_OUT_OF_ORDER
+    }
+    // the LDS exchange only once some entry of the wave has failed (wave-uniform flag)
+    if (__ballot(key != ~0u)) anyfail = true;
+    if (anyfail) {
       if (key != ~0u)
         __hip_atomic_fetch_min(&fkw[wave0 + o], key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+      __builtin_amdgcn_wave_barrier();
     }
-    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-    __builtin_amdgcn_wave_barrier();
     // phase 2: entries below the owner's first failure are applied
     if (mine) {
-      const uint32_t fk = fkw[wave0 + o];
+      const uint32_t fk = anyfail ? fkw[wave0 + o] : ~0u;
       const uint32_t f = fk == ~0u ? ~0u : fk >> 2;
       if (i < f && i >= olen)  // i == len in node_apply's walk: appended
         D.stor[(size_t)oc * D.apply_cap + i] = SE{e.val, s.mask | (1u << ome), e.term};
@@ -871,12 +881,14 @@ DI void node_apply_coop(const Dev& D, X& x, uint32_t me, NC& d) {
         }
       }
     }
-    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-    __builtin_amdgcn_wave_barrier();
+    if (snapmode || anyfail) {  // LDS writes (snapshot term) / reads done before the next round
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+    }
   }
   if (!cnt) return;
   // the owner: counters and node state as node_apply leaves them
-  const uint32_t fk = fkw[threadIdx.x];
+  const uint32_t fk = anyfail ? fkw[threadIdx.x] : ~0u;
   const uint32_t end = fk == ~0u ? d.commit : (fk >> 2) - 1u;  // last entry applied in full
   const uint32_t napplied = end + 1u - base;                    // may be 0 (f == base)
   CADD(CNT_APPLIES, napplied + (fk != ~0u && (fk & 3u) != 0u ? 1u : 0u));
@@ -963,8 +975,8 @@ DI uint32_t on_ack(const Dev& D, X& x, uint32_t me, NC& d, uint32_t p, uint32_t 
 // AC entries j.. of an AppendEntries payload (the sender's ring, or the
 // materialized copy) and the receiver's entries at their indices: their terms, and (MR_F_SAFETY
 // log matching) their commands, from one 16-B load per entry
-#ifndef MR_AE_OWN
-#define MR_AE_OWN 1
+#ifndef MR_AE_OWN  // 5-server kernels: yes (+0.7 %); 7 / 8: no (118 -> 4 spilled VGPRs at NB = 7)
+#define MR_AE_OWN (MR_NB <= 5)
 #endif
 DI void ae_load_batch(const Dev& D, const X& x, uint32_t me, const NC& d, uint32_t src, bool mat,
                       const LE* pp, uint32_t ma, uint32_t k, uint32_t j, LE (&pe)[AC],
@@ -982,9 +994,14 @@ DI void ae_load_batch(const Dev& D, const X& x, uint32_t me, const NC& d, uint32
     ov[q] = o.val;
     ors[q] = o.rs;
 #else
-    lt[q] = (jx < k && i <= d.last) ? term_at(D, x, me, d, i) : 0u;
+    // (term, rs) of our entry at i as one 8-B load (i > snap, see above); the MR_F_SAFETY
+    // log-matching check loads the commands separately
+    const bool own = jx < k && i <= d.last;
+    const uint2 tr = (own && i != d.last) ? *reinterpret_cast<const uint2*>(&D.log[logi(D, x, me, i)])
+                                          : make_uint2(0u, 0u);
+    lt[q] = own ? (i == d.last ? d.lastt : tr.x) : 0u;
     ov[q] = 0;
-    ors[q] = (jx < k && i < d.last && i > d.snap) ? D.log[logi(D, x, me, i)].rs : 0u;
+    ors[q] = tr.y;
 #endif
   }
 }
@@ -1432,7 +1449,11 @@ DI void t_new(const Dev& D, X& x, bool snapshot) {  // RaftTester::new, tester.r
 }
 // bit mask of the servers whose role is leader: one batch of independent loads
 // (a start() changes only its own server, so a loop of starts can use it)
+#ifndef MR_LMASK
+#define MR_LMASK 1
+#endif
 DI uint32_t t_leaders(const Dev& D, X& x) {
+  if (MR_LMASK) return x.lmask;
   uint32_t m = 0;
 #pragma unroll
   for (uint32_t i = 0; i < NB; i++)
@@ -1445,13 +1466,19 @@ DI bool t_start(const Dev& D, X& x, uint32_t i, uint64_t v, uint32_t& idx, uint3
                 bool lead) {
   if (!bit(x.alive, i)) { fail(D, x, MR_FAIL_UNWRAP_NONE); return false; }
   if (D.null_raft || !lead) return false;  // Err(NotLeader((me+1)%n))
-  uint32_t snap = ND(NF_SNAP, i), last = ND(NF_LAST, i) + 1;
+  // words 0..15 of the record (scalars, pending payload range) and rs(last) as one batch of
+  // independent loads: the write guard below needs no further round trip
+  const uint4* rp = reinterpret_cast<const uint4*>(NDP(i));
+  const uint4 r0 = rp[0], r1 = rp[1], r2 = rp[2];
+  const uint2 pr = reinterpret_cast<const uint2*>(NDP(i))[NF_PLO / 2];
+  const uint32_t lrs = LRS(i);
+  const uint32_t snap = r1.y, last = r1.x + 1;
   if (last - snap > D.log_cap) { fail(D, x, MR_FAIL_SIM_CAPACITY); return false; }
   size_t li = logi(D, x, i, last);
-  term = ND(NF_TERM, i);
-  uint32_t pexp = ND(NF_PEXP, i);
-  const uint32_t rs = term == ND(NF_LASTT, i) ? LRS(i) : last;  // run start (le_at)
-  guard_log_write(D, x, i, pexp, last);
+  term = r0.y;
+  uint32_t pexp = r2.y;
+  const uint32_t rs = term == r2.w ? lrs : last;  // run start (le_at)
+  guard_log_write(D, x, i, pexp, last, pr.x, pr.y);
   ND(NF_PEXP, i) = pexp;
   D.log[li] = LE{term, rs, v};
   LRS(i) = rs;
@@ -1462,8 +1489,47 @@ DI bool t_start(const Dev& D, X& x, uint32_t i, uint64_t v, uint32_t& idx, uint3
   idx = last;
   return true;
 }
+// `count` start(gen_entry()) calls on server i in a row with nothing between them (snap_common's
+// burst, tests.rs:889-892): the record is loaded once and stored once, the appends in between
+// are the same as `count` t_start calls (each draw precedes its start; a failure stops there)
+DI uint64_t t_entry_for_start(const Dev& D, X& x, uint32_t i, uint32_t lm);
+DI void t_start_burst(const Dev& D, X& x, uint32_t i, uint32_t count) {
+  const uint32_t lm = t_leaders(D, x);
+  const bool go = bit(x.alive, i) && !D.null_raft && bit(lm, i);
+  uint4 r0 = make_uint4(0u, 0u, 0u, 0u), r1 = r0, r2 = r0;
+  uint2 pr = make_uint2(0u, 0u);
+  uint32_t lrs = 0;
+  if (go) {
+    const uint4* rp = reinterpret_cast<const uint4*>(NDP(i));
+    r0 = rp[0]; r1 = rp[1]; r2 = rp[2];
+    pr = reinterpret_cast<const uint2*>(NDP(i))[NF_PLO / 2];
+    lrs = LRS(i);
+  }
+  const uint32_t term = r0.y, snap = r1.y;
+  uint32_t last = r1.x, lastt = r2.w, pexp = r2.y;
+  for (uint32_t k = 0; k < count; k++) {
+    const uint64_t v = t_entry_for_start(D, x, i, lm);
+    if (!bit(x.alive, i)) { fail(D, x, MR_FAIL_UNWRAP_NONE); return; }
+    if (!go) continue;  // Err(NotLeader)
+    const uint32_t idx = last + 1;
+    if (idx - snap > D.log_cap) { fail(D, x, MR_FAIL_SIM_CAPACITY); return; }
+    guard_log_write(D, x, i, pexp, idx, pr.x, pr.y);  // pexp = 0 after a materialize
+    const uint32_t rs = term == lastt ? lrs : idx;
+    D.log[logi(D, x, i, idx)] = LE{term, rs, v};
+    CADD(CNT_LOG_WRITES, 1u);
+    CMAX(CNT_MAX_LOG, idx - snap);
+    last = idx;
+    lastt = term;
+    lrs = rs;
+  }
+  if (!go) return;
+  ND(NF_PEXP, i) = pexp;
+  ND(NF_LAST, i) = last;
+  ND(NF_LASTT, i) = lastt;
+  LRS(i) = lrs;
+}
 DI bool t_start(const Dev& D, X& x, uint32_t i, uint64_t v, uint32_t& idx, uint32_t& term) {
-  return t_start(D, x, i, v, idx, term, f_role(ND(NF_FLAGS, i)) == R_L);
+  return t_start(D, x, i, v, idx, term, bit(t_leaders(D, x), i) != 0u);
 }
 DI bool t_start(const Dev& D, X& x, uint32_t i, uint64_t v) {
   uint32_t a, b;
@@ -1497,7 +1563,7 @@ DI void t_check_no_leader(const Dev& D, X& x) {  // tester.rs:112-122
   for (uint32_t i = 0; i < D.n; i++) {
     if (!bit(x.conn, i)) continue;
     if (!bit(x.alive, i)) { fail(D, x, MR_FAIL_UNWRAP_NONE); return; }
-    if (!D.null_raft && f_role(ND(NF_FLAGS, i)) == R_L) {
+    if (!D.null_raft && bit(t_leaders(D, x), i)) {
       fail(D, x, MR_FAIL_UNEXPECTED_LEADER);
       return;
     }
@@ -1583,7 +1649,7 @@ DI void lane_load(const Dev& D, X& x) {
   x.now = CS(CS_NOW); x.events = CS(CS_EVENTS); x.msgs_sent = CS(CS_MSGS);
   x.inflight = CS(CS_INFLIGHT); x.trace_n = CS(CS_TRACEN); x.mslot = CS(CS_MSLOT);
   x.netmode = CS(CS_NETMODE); x.t_ctr = CS(CS_TCTR);
-  x.conn = CS(CS_CONN); x.alive = CS(CS_ALIVE); x.twake = CS(CS_TWAKE);
+  x.conn = CS(CS_CONN); x.alive = CS(CS_ALIVE); x.twake = CS(CS_TWAKE); x.lmask = CS(CS_LMASK);
   if constexpr (nthr(S) > 0) { x.cwake = CS(CS_CWAKE); x.ctid = CS(CS_CTID); x.cslot = CS(CS_CSLOT); }
 #pragma unroll
   for (uint32_t d = 0; d < NB; d++) x.timer[d] = d < D.n ? TMR(d) : INF_T;
@@ -1603,7 +1669,7 @@ DI void lane_store(const Dev& D, X& x) {
   CS(CS_NOW) = x.now; CS(CS_EVENTS) = x.events; CS(CS_MSGS) = x.msgs_sent;
   CS(CS_INFLIGHT) = x.inflight; CS(CS_TRACEN) = x.trace_n; CS(CS_MSLOT) = x.mslot;
   CS(CS_NETMODE) = x.netmode; CS(CS_TCTR) = x.t_ctr;
-  CS(CS_CONN) = x.conn; CS(CS_ALIVE) = x.alive; CS(CS_TWAKE) = x.twake;
+  CS(CS_CONN) = x.conn; CS(CS_ALIVE) = x.alive; CS(CS_TWAKE) = x.twake; CS(CS_LMASK) = x.lmask;
   if constexpr (nthr(S) > 0) { CS(CS_CWAKE) = x.cwake; CS(CS_CTID) = x.ctid; CS(CS_CSLOT) = x.cslot; }
 #pragma unroll
   for (uint32_t d = 0; d < NB; d++)
