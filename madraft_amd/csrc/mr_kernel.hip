@@ -93,9 +93,22 @@ struct X {
 constexpr uint32_t STEP_BLOCK = MW > 2 ? 64 : MR_BLOCK;
 // MR_KEY32: a 32-bit LDS key t << 5 | dst (t < 2^27 - 1, SEMANTICS §4); the (rare) tie of
 // two messages at the same t is broken by their sequence numbers, kept in the message
-// record (word MF_PAD). Otherwise a 64-bit key (t << 32 | seq << 5 | dst).
+// record (word MF_PAD). Otherwise a 64-bit key (t << 32 | seq << 6 | ae << 5 | dst).
 #ifndef MR_KEY32
 #define MR_KEY32 0
+#endif
+#ifndef MR_AE_CLASS  // AppendEntries deliveries as a sub-class of the node events (step_kernel)
+#define MR_AE_CLASS 1
+#endif
+#ifndef MR_AE_NUM  // A/B: 1/2 135.4 ms, 1/3 136.1, 1/4 138.2, 2/3 139.3, off 144.7
+#define MR_AE_NUM 1
+#define MR_AE_DEN 2
+#endif
+#ifndef MR_AE_K0  // heartbeats (no entries) in the AE sub-class too
+#define MR_AE_K0 1
+#endif
+#ifndef MR_HB_CLASS  // leaders' heartbeat timers as a sub-class of their own (same rule)
+#define MR_HB_CLASS 0
 #endif
 using lkey_t = std::conditional_t<MR_KEY32 != 0, uint32_t, uint64_t>;
 constexpr lkey_t LKEY_FREE = ~lkey_t(0);
@@ -487,7 +500,7 @@ DI int net_send(const Dev& D, X& x, uint32_t src, uint32_t& nctr, uint32_t dst, 
     fail(D, x, MR_FAIL_SIM_CAPACITY);
     return -1;
   }
-  if (seq >= (1u << 25)) { fail(D, x, MR_FAIL_SIM_CAPACITY); return -1; }  // SEMANTICS §3, §9
+  if (seq >= (1u << 24)) { fail(D, x, MR_FAIL_SIM_CAPACITY); return -1; }  // SEMANTICS §3, §9
   uint32_t t = x.now + u_range(w1, 1000u, net_lat_hi(x));
   if (t >= T_KEY_MAX) { fail(D, x, MR_FAIL_SIM_CAPACITY); return -1; }  // SEMANTICS §4
   uint32_t slot = 0;
@@ -517,7 +530,10 @@ DI int net_send(const Dev& D, X& x, uint32_t src, uint32_t& nctr, uint32_t dst, 
     // every message in flight has a smaller seq: a new one is earliest only by time
     if (t < (uint32_t)(x.mmin >> 32)) { x.mmin = ((uint64_t)t << 32) | dst; x.mslot = slot; }
   } else {
-    const uint64_t key = ((uint64_t)t << 32) | (seq << 5) | dst;
+    // bit 5: AppendEntries request (the step loop's AE sub-class, MR_AE_CLASS); below the
+    // unique seq, so it never decides the order
+    const uint64_t key = ((uint64_t)t << 32) | (seq << 6) |
+                         (type == M_AE_REQ && (MR_AE_K0 || k) ? 32u : 0u) | dst;
     LK(slot) = key;
     if (key < x.mmin) { x.mmin = key; x.mslot = slot; }
   }
@@ -1778,10 +1794,25 @@ __global__ void __launch_bounds__(STEP_BLOCK, step_waves<S>()) step_kernel(Dev D
     const bool tpick = MR_TESTER_DEN * ns >= MR_TESTER_NUM * (nm + nt + ns);
     const uint32_t pick = tpick ? CLS_TESTER : (nm >= nt ? CLS_MSG : CLS_TIMER);
 #ifdef MR_ALL_CLASSES  // experiment: every lane runs its own event (divergent paths)
-    const bool mine = true;
+    bool mine = true;
 #else
-    const bool mine = MR_MERGE_NODE ? (tpick ? cls == CLS_TESTER : cls != CLS_TESTER) : cls == pick;
+    bool mine = MR_MERGE_NODE ? (tpick ? cls == CLS_TESTER : cls != CLS_TESTER) : cls == pick;
 #endif
+    // AppendEntries deliveries (the longest node path: probe, payload batches, log writes) wait
+    // until they are >= AE_NUM / AE_DEN of the wave's node events, so the other node events run
+    // without their round trips; like any lane that waits, a cluster's own order is unchanged
+    if constexpr (MR_AE_CLASS && !MR_KEY32) {
+      if (!tpick) {
+        const bool ae = run && cls == CLS_MSG && ((key >> 5) & 1u);
+        const uint32_t nae = __popcll(__ballot(ae));
+        if (nae < nm + nt && MR_AE_DEN * nae < MR_AE_NUM * (nm + nt)) mine = mine && !ae;
+        if constexpr (MR_HB_CLASS) {
+          const bool hb = run && cls == CLS_TIMER && bit(x.lmask, node);
+          const uint32_t nhb = __popcll(__ballot(hb));
+          if (nhb < nm + nt && MR_AE_DEN * nhb < MR_AE_NUM * (nm + nt)) mine = mine && !hb;
+        }
+      }
+    }
     PROF(P_SEL);
     if (!run || !mine) continue;
     if (nthr(S) > 0 && (uint32_t)(key >> 32) == INF_T) {  // nothing can wake the test body
@@ -1796,7 +1827,7 @@ __global__ void __launch_bounds__(STEP_BLOCK, step_waves<S>()) step_kernel(Dev D
       CADD(cls == CLS_MSG ? CNT_EV_MSG : CNT_EV_TIMER, 1u);
       NR nr;
       nr.on = false;
-      node_event<S>(D, x, cls == CLS_MSG, node, x.mslot, ((uint32_t)key & 0x3FFFFFFFu) >> 5, nr);
+      node_event<S>(D, x, cls == CLS_MSG, node, x.mslot, ((uint32_t)key & 0x3FFFFFFFu) >> 6, nr);
       if (MR_REC_ONCE && nr.on && x.code == RUN)
         rec8(D, x, x.now, nr.w1, nr.aux, nr.term, nr.commit, nr.applied, nr.last, nr.snap);
     } else {

@@ -320,7 +320,7 @@ static void net_send(OSim* s, uint32_t src, uint32_t dst, OMsg* m) {
   if (w[0] < s->loss) { s->r.drop_loss++; return; }
   /* madsim's net has no in-flight cap: a full slot table is a simulator limit, not loss */
   if (s->inflight >= s->cfg.msg_slots) { s->r.drop_overflow++; t_fail(s, MR_FAIL_SIM_CAPACITY); }
-  if (seq >= (1u << 25)) t_fail(s, MR_FAIL_SIM_CAPACITY); /* SEMANTICS §3, §9 */
+  if (seq >= (1u << 24)) t_fail(s, MR_FAIL_SIM_CAPACITY); /* SEMANTICS §3, §9 */
   m->time = s->now + u_range(w[1], s->lat_lo, s->lat_hi);
   if (m->time >= (1u << 27) - 1u) t_fail(s, MR_FAIL_SIM_CAPACITY); /* SEMANTICS §4: t < 2^27 - 1 */
   m->seq = seq; m->src = (uint8_t)src; m->dst = (uint8_t)dst;
