@@ -97,7 +97,10 @@ constexpr uint32_t STEP_BLOCK = MW > 2 ? 64 : MR_BLOCK;
 #ifndef MR_KEY32
 #define MR_KEY32 0
 #endif
-#ifndef MR_AE_CLASS  // AppendEntries deliveries as a sub-class of the node events (step_kernel)
+// AppendEntries deliveries as a sub-class of the node events (step_kernel), a scheduling
+// policy chosen per scenario by A/B (profiles/r02_ab_configs.txt): figure_8_unreliable_2c
+// +6.5 %; its crash variant -8.5 %, kvraft unreliable_3a -6.7 %, fail_agree_2b 0: off there
+#ifndef MR_AE_CLASS
 #define MR_AE_CLASS 1
 #endif
 #ifndef MR_AE_NUM  // A/B: 1/2 135.4 ms, 1/3 136.1, 1/4 138.2, 2/3 139.3, off 144.7
@@ -1801,7 +1804,7 @@ __global__ void __launch_bounds__(STEP_BLOCK, step_waves<S>()) step_kernel(Dev D
     // AppendEntries deliveries (the longest node path: probe, payload batches, log writes) wait
     // until they are >= AE_NUM / AE_DEN of the wave's node events, so the other node events run
     // without their round trips; like any lane that waits, a cluster's own order is unchanged
-    if constexpr (MR_AE_CLASS && !MR_KEY32) {
+    if constexpr (MR_AE_CLASS && !MR_KEY32 && S == MR_SCN_FIGURE_8_UNRELIABLE_2C) {
       if (!tpick) {
         const bool ae = run && cls == CLS_MSG && ((key >> 5) & 1u);
         const uint32_t nae = __popcll(__ballot(ae));
