@@ -119,9 +119,11 @@ constexpr uint32_t tok_letter(char c) { return (1u << 20) + (uint32_t)(c - 'A');
 constexpr uint32_t CHURN_VCAP = 512;  // values one churn client may record (tests.rs:763-797)
 // kv32 [C][n][KVREC]: per-server KV state (SEMANTICS §9): dedup[clerk] at 0..127, pending
 // request p at 128 + 8p: {index (0 = free), clerk | ready << 8 | status << 9 | host << 16,
-// seq, tag, value, hash lo, hash hi, -}, the shard_ctrler config count at 192, and key k at
-// 256 + 8k: {hash lo, hash hi, byte length, appender 0..4 (cli + 1 | count << 8 | bad << 31)}
-constexpr uint32_t KVR_DEDUP = 0, KVR_PEND = 128, KVR_NCFG = 192, KVR_KEYS = 256, KVREC = 768;
+// seq, tag, value, hash lo, hash hi, -}, the shard_ctrler config count at 192, the mask of
+// occupied pending slots at 193, and key k at 256 + 8k: {hash lo, hash hi, byte length,
+// appender 0..4 (cli + 1 | count << 8 | bad << 31)}
+constexpr uint32_t KVR_DEDUP = 0, KVR_PEND = 128, KVR_NCFG = 192, KVR_PMASK = 193, KVR_KEYS = 256,
+                   KVREC = 768;
 constexpr uint32_t KV_KEYS = 64, KV_KW = 8, KV_APP = 5, MAX_CLERKS = 128;
 constexpr uint32_t KV_ALL = 0xFFFFFFu;  // Get elem: appenders 0..4, packed
 constexpr uint64_t KV_HP = 0x100000001B3ull;  // value hash multiplier

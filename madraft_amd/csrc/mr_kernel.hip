@@ -671,6 +671,8 @@ DI void node_apply(const Dev& D, X& x, uint32_t me, NC& d, bool& kvready) {
   const bool snapmode = (x.netmode >> 1) & 1u;
   SE* const sb = D.stor + (size_t)x.c * D.apply_cap;
   uint32_t len = d.slen;
+  uint32_t pm = 0;  // KV: the server's occupied pending-request slots (kv_apply)
+  if constexpr (KV) pm = KVP(me)[KVR_PMASK];
 #if MR_AP_PIPE
   // software-pipelined: batch b + 1's loads are issued before batch b's checker stores, so
   // they do not wait behind them on vmcnt (disjoint indices: a batch never reads what an
@@ -720,7 +722,7 @@ DI void node_apply(const Dev& D, X& x, uint32_t me, NC& d, bool& kvready) {
         CADD(CNT_SNAPSHOTS, 1u);
       }
       if constexpr (KV) {
-        kv_apply<is_ctrl(S)>(D, x, me, i, ce[j].val, kvready);
+        kv_apply<is_ctrl(S)>(D, x, me, i, ce[j].val, kvready, pm);
         if (x.code != RUN) return;
       }
       if constexpr (kv_gen(S).maxraft > 0) {  // the KV service snapshots (SEMANTICS §9)
@@ -774,7 +776,7 @@ DI void node_apply(const Dev& D, X& x, uint32_t me, NC& d, bool& kvready) {
         CADD(CNT_SNAPSHOTS, 1u);
       }
       if constexpr (KV) {
-        kv_apply<is_ctrl(S)>(D, x, me, i, e[j].val, kvready);
+        kv_apply<is_ctrl(S)>(D, x, me, i, e[j].val, kvready, pm);
         if (x.code != RUN) return;
       }
       if constexpr (kv_gen(S).maxraft > 0) {  // the KV service snapshots (SEMANTICS §9)
@@ -1448,6 +1450,7 @@ DI void t_crash1(const Dev& D, X& x, uint32_t i) {  // tester.rs:329-333
   if (D.kv32) {  // its RPC handler tasks die with it: pending requests are dropped
     uint4* pp = reinterpret_cast<uint4*>(D.kv32 + ((size_t)x.c * D.n + i) * KVREC + KVR_PEND);
     for (uint32_t p = 0; p < 2 * KV_PEND; p++) pp[p] = make_uint4(0u, 0u, 0u, 0u);
+    D.kv32[((size_t)x.c * D.n + i) * KVREC + KVR_PMASK] = 0u;
   }
 }
 DI void t_start1(const Dev& D, X& x, uint32_t i) {  // tester.rs:293-327, raft.rs:108-122
