@@ -626,6 +626,9 @@ constexpr uint32_t AC = MR_AC;  // entries per batch of independent loads in log
 #ifndef MR_AP_PIPE  // software-pipelined applier batches (node_apply); A/B in DESIGN.md §6
 #define MR_AP_PIPE 1
 #endif
+#ifndef MR_KV_PRE  // KV applier: a batch's key records loaded with the batch (node_apply)
+#define MR_KV_PRE 0
+#endif
 #ifndef MR_AC_APPLY  // pipelined: two batches of 5 in flight fit the registers (8: spills)
 #define MR_AC_APPLY (MR_AP_PIPE ? 5 : 8)
 #endif
@@ -700,6 +703,28 @@ DI void node_apply(const Dev& D, X& x, uint32_t me, NC& d, bool& kvready) {
 #pragma unroll
     for (uint32_t j = 0; j < AC_APPLY; j++) { ce[j] = e[j]; cm[j] = m[j]; csv[j] = sv[j]; }
     if (i0 + AC_APPLY <= d.commit) load_batch(i0 + AC_APPLY);
+    // KV (not the controller): the batch's key records and dedup words as one batch of loads
+    // (the batch's commands are known here); an entry whose key or clerk an earlier entry of
+    // the batch shares reads them after that entry's stores instead (kv_apply loads)
+    constexpr bool PRE = KV && !is_ctrl(S) && MR_KV_PRE;
+    uint4 pka[AC_APPLY], pkb[AC_APPLY];
+    uint32_t pdd[AC_APPLY], pkey[AC_APPLY], pcl[AC_APPLY];
+    if constexpr (PRE) {
+      const uint32_t* kp = KVP(me);
+#pragma unroll
+      for (uint32_t j = 0; j < AC_APPLY; j++) {
+        const uint32_t i = i0 + j;
+        const bool ok = i <= d.commit && i < D.apply_cap;
+        const uint64_t v = ce[j].val;
+        const uint32_t key = (uint32_t)(v >> 55) & 63u, cl = (uint32_t)(v >> 48) & 127u;
+        pkey[j] = ok ? key : 64u + j;  // no match for entries past the batch
+        pcl[j] = ok ? cl : 128u + j;
+        const uint4* kq = reinterpret_cast<const uint4*>(kp + KVR_KEYS + KV_KW * key);
+        pka[j] = ok ? kq[0] : uint4{};
+        pkb[j] = ok ? kq[1] : uint4{};
+        pdd[j] = ok ? kp[KVR_DEDUP + cl] : 0u;
+      }
+    }
     PROF(P_AP_LOAD);
 #pragma unroll
     for (uint32_t j = 0; j < AC_APPLY; j++) {
@@ -722,7 +747,14 @@ DI void node_apply(const Dev& D, X& x, uint32_t me, NC& d, bool& kvready) {
         CADD(CNT_SNAPSHOTS, 1u);
       }
       if constexpr (KV) {
-        kv_apply<is_ctrl(S)>(D, x, me, i, ce[j].val, kvready, pm);
+        bool pre = false;
+        if constexpr (PRE) {
+          bool conf = false;
+#pragma unroll
+          for (uint32_t q = 0; q < j; q++) conf |= pkey[q] == pkey[j] || pcl[q] == pcl[j];
+          pre = !conf;
+        }
+        kv_apply<is_ctrl(S)>(D, x, me, i, ce[j].val, kvready, pm, pre, pka[j], pkb[j], pdd[j]);
         if (x.code != RUN) return;
       }
       if constexpr (kv_gen(S).maxraft > 0) {  // the KV service snapshots (SEMANTICS §9)
