@@ -86,9 +86,9 @@ struct X {
 // message keys of the lane's cluster live in LDS during a launch: [slot][lane],
 // so a wave's 64 lanes read 64 consecutive u64 (conflict-free). Free slots hold
 // ~0, so the earliest-message scan is a branch-free min over all M slots.
-// lanes per block: 128, or 64 where 256 slots of keys must fit the 160 KiB of LDS
+// lanes per block: 64 (A/B below; 256 message slots of keys need it to fit the 160 KiB of LDS)
 #ifndef MR_BLOCK
-#define MR_BLOCK 128
+#define MR_BLOCK 64  // A/B round 2 (with AC 4): configs 2-4 +2.4-10 %, config 5 -1 % (r02_s2r)
 #endif
 constexpr uint32_t STEP_BLOCK = MW > 2 ? 64 : MR_BLOCK;
 // MR_KEY32: a 32-bit LDS key t << 5 | dst (t < 2^27 - 1, SEMANTICS §4); the (rare) tie of
@@ -614,7 +614,7 @@ DI void guard_log_write(const Dev& D, X& x, uint32_t L, uint32_t& pexp, uint32_t
 
 // ---------------------------------------------------------------- tester storage
 #ifndef MR_AC
-#define MR_AC 8
+#define MR_AC 4  // A/B round 2: 4 vs 8 +1.7 % figure_8 with 64-lane blocks (profiles/r02_ab_configs.txt r02_s2r)
 #endif
 constexpr uint32_t AC = MR_AC;  // entries per batch of independent loads in log walks
 #ifndef MR_SEND_EARLY  // a leader's append-term loads issued before the applier (A/B in DESIGN.md §6)
