@@ -82,18 +82,41 @@ def cpu_baseline(test, seeds_per_proc, procs, safety=False):
                       f"MADSIM_TEST_NUM={seeds_per_proc} each)"}
 
 
-def load_pmc(test, clusters):
-    """HBM traffic per step-kernel launch from the committed rocprofv3 --pmc
-    summary of the same workload (profiles/pmc_*.json, newest round last), or None."""
-    best = None
+def load_pmc(test, clusters, lib_sha):
+    """HBM traffic per step-kernel launch from the committed rocprofv3 --pmc summary
+    (profiles/pmc_*.json, tools/pmc_sum.py) of THIS library build on this workload: the record
+    whose lib_sha16 equals the loaded library's, else None (the bench then reports traffic null
+    rather than a figure measured on another build)."""
     for p in sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc_*.json"))):
         try:
             d = json.load(open(p))
         except (OSError, ValueError):
             continue
-        if d.get("test") == test and d.get("clusters") == clusters and d.get("abi", 2) >= 3:
-            best = d
-    return best
+        if (d.get("test") == test and d.get("clusters") == clusters
+                and d.get("lib_sha16") == lib_sha):
+            d["file"] = os.path.relpath(p, ROOT)
+            return d
+    return None
+
+
+def host_cores():
+    """CPUs this process may run on (sched_getaffinity), and the cgroup CPU quota in cores
+    if one is set (cpu.max / cfs_quota_us), else None."""
+    n = len(os.sched_getaffinity(0))
+    quota = None
+    for qf, pf in (("/sys/fs/cgroup/cpu.max", None),
+                   ("/sys/fs/cgroup/cpu/cpu.cfs_quota_us", "/sys/fs/cgroup/cpu/cpu.cfs_period_us")):
+        try:
+            if pf is None:
+                q, p = open(qf).read().split()[:2]
+            else:
+                q, p = open(qf).read().strip(), open(pf).read().strip()
+            if q not in ("max", "-1"):
+                quota = round(int(q) / int(p), 2)
+            break
+        except (OSError, ValueError):
+            continue
+    return n, quota
 
 
 def relaunch(gpus):
@@ -143,7 +166,8 @@ def main():
     ap.add_argument("--variant", default="figure_8_unreliable_crash",
                     help="second workload timed on the same shard ('' = none)")
     ap.add_argument("--variant-steps", type=int, default=2)
-    ap.add_argument("--cpu-seeds", type=int, default=20000, help="cpu_baseline seeds per process")
+    ap.add_argument("--cpu-seeds", type=int, default=320000,
+                    help="cpu_baseline sample: seeds in total, split over one process per core")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-safety", action="store_true",
                     help="without the per-event Raft invariant checks (MR_F_SAFETY)")
@@ -193,7 +217,8 @@ def main():
     r0_bytes = alg_bytes(r0, n)
     kern_s = r0["kernel_ms"] / 1000.0
     achieved = r0_bytes / kern_s / 1e9 if kern_s > 0 else 0.0
-    pmc = load_pmc(a.test, a.clusters)
+    lib_sha = sim.lib_sha16()
+    pmc = load_pmc(a.test, a.clusters, lib_sha)
     traffic = pmc.get("hbm_bytes_per_launch") if pmc else None
     per_launch = r0_bytes / max(r0["launches"], 1)
     out = {
@@ -221,6 +246,9 @@ def main():
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
                      "traffic": traffic,
                      "traffic_over_alg": round(traffic / per_launch, 3) if traffic else None,
+                     "traffic_source": (f"{pmc['file']} (lib {lib_sha}, FETCH_SIZE x "
+                                        f"{pmc.get('fetch_factor', 2)} + WRITE_SIZE)")
+                                       if pmc else f"no PMC record of lib {lib_sha} on this workload",
                      "kernel": "step_kernel",
                      "launches": r0["launches"],
                      "avg_launch_ms": round(r0["kernel_ms"] / max(r0["launches"], 1), 4),
@@ -230,6 +258,7 @@ def main():
                               "enqueued / delivered, 16 B per entry read at delivery / written, "
                               "48 B per apply)"},
         "alg_bytes_total": alg_bytes(tot, n),
+        "lib_sha16": lib_sha,
     }
     if a.variant:
         bv = sim.Batch(a.variant, count, _abi.README_SEED, cluster_base=base, device=local,
@@ -251,9 +280,11 @@ def main():
             "note": "config 3 read literally: crash1/start1 + persister (tests.rs:612-660) in "
                     "figure_8_unreliable's loop"}}
     if rank == 0 and not a.no_cpu_baseline:
-        procs = min(16, os.cpu_count() or 1)
-        test = a.test
-        out["cpu_baseline"] = cpu_baseline(test, a.cpu_seeds, procs, safety=not a.no_safety)
+        procs, quota = host_cores()  # one process per host core (north_star), all of them
+        per = max(100, -(-a.cpu_seeds // procs))
+        out["cpu_baseline"] = cpu_baseline(a.test, per, procs, safety=not a.no_safety)
+        if quota is not None:
+            out["cpu_baseline"]["cgroup_cpu_quota_cores"] = quota
         out["gpu_over_cpu"] = round(out["value"] / out["cpu_baseline"]["value"], 2)
     if rank == 0:
         print(json.dumps(out), flush=True)

@@ -29,7 +29,7 @@ def main():
         flags |= {"vote_twice": _abi.MR_F_BUG_VOTE_TWICE, "vote_stale": _abi.MR_F_BUG_VOTE_STALE,
                   "no_prev_check": _abi.MR_F_BUG_NO_PREV_CHECK}[a.bug]
     if a.replay:
-        tr, code, tm, misses = sim.replay(a.test, trace.load_jsonl(a.replay), seed=a.seed or _abi.README_SEED,
+        tr, code, tm, misses = sim.replay(a.test, trace.load_jsonl(a.replay, unreliable=True if a.unreliable else None), seed=a.seed or _abi.README_SEED,
                                           nodes=a.nodes, iters=a.iters, unreliable=a.unreliable,
                                           null_raft=a.null, safety=a.safety, flags=flags)
         print(json.dumps({"code": code, "verdict": _abi.FAIL_NAMES.get(code, str(code)),

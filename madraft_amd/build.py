@@ -77,11 +77,12 @@ def _units(csrc, scns=None):
     return units
 
 
-def build_hip(force=False, verbose=False, extra=(), out=None, scns=None):
-    """Compile the product library; `extra` flags / `out` path / only scenario ids `scns`
-    for dev variants."""
+def build_hip(force=False, verbose=False, extra=(), out=None, scns=None, csrc=None):
+    """Compile the product library; `extra` flags / `out` path / only scenario ids `scns` /
+    another source tree `csrc` (a snapshot laid out as madraft_amd/csrc + include/) for dev
+    variants."""
     out = out or LIB
-    csrc = os.path.join(HERE, "csrc")
+    csrc = csrc or os.path.join(HERE, "csrc")
     srcs = sorted(glob.glob(os.path.join(csrc, "*.hip")) + glob.glob(os.path.join(csrc, "*.cpp")))
     deps = srcs + glob.glob(os.path.join(csrc, "*.h")) + glob.glob(os.path.join(csrc, "*.inc")) + \
         [os.path.join(ROOT, "include", "madraft_sim.h"), os.path.abspath(__file__)]

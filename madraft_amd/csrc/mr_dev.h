@@ -171,8 +171,11 @@ struct Dev {
   uint32_t* kv32;   // [C][n][KVREC]        (kvraft only)
   uint32_t* kvs32;  // [C][n][KVS_W]        persisted KV snapshots (maxraftstate)
   uint32_t* kring;  // [C][KV_RING][KRW]    recent KV snapshots by index (maxraftstate)
-  uint4* dtab;      // [C][dcap] keyed decisions {stream << 16 | entity, seq, w0, w1}, else null
-  uint32_t dcap;       // replay: a power of two, each row sorted by key and padded with ~0
+  uint4* dtab;      // keyed decisions {stream << 16 | entity, seq, w0, w1}, else null:
+                    // replay: CSR rows, cluster c's sorted by key at [doff[c], doff[c + 1]);
+                    // record: [C][dcap], appended in draw order
+  uint32_t* doff;   // replay: [C + 1] row offsets into dtab
+  uint32_t dcap;       // record: decisions kept per cluster
   uint32_t tape_mode;  // 0 Philox, 1 replay keyed decisions, 2 Philox and record them
   uint64_t* cval;   // [C][3][CHURN_VCAP]   churn clients' committed values (churn only)
   uint32_t* cidx;   // [C][3][CHURN_VCAP]   ... and the index each was seen at
@@ -257,6 +260,12 @@ constexpr uint32_t nb_of(uint32_t s) { return k_default_n[s] <= 5 ? k_default_n[
 // scenarios with a 7-server instance as well (BASELINE config 4 runs the 2D tests with 7
 // servers; arrays sized for 7 keep fewer registers live than the 8-server instance)
 constexpr bool has_nb7(uint32_t s) {
+  return s >= MR_SCN_SNAPSHOT_BASIC_2D && s <= MR_SCN_SNAPSHOT_INSTALL_UNRELIABLE_CRASH_2D;
+}
+// scenarios whose test body starts the tester with service snapshots (t_new(snapshot = true),
+// tester.rs:303-325 SNAPSHOT_INTERVAL): snap_common's five 2D tests. node_apply_coop specializes
+// on it at compile time and checks it against the runtime mode (x.netmode bit 1).
+constexpr bool uses_service_snapshots(uint32_t s) {
   return s >= MR_SCN_SNAPSHOT_BASIC_2D && s <= MR_SCN_SNAPSHOT_INSTALL_UNRELIABLE_CRASH_2D;
 }
 #define MR_ALL_SCNS                                                                       \

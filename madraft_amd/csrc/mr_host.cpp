@@ -110,6 +110,7 @@ struct mr_batch {
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   uint32_t budget = 16384;  // events per cluster per launch (MR_STEP_BUDGET)
   uint4* tape = nullptr;     // keyed decisions (own allocation: set_decisions / MR_F_RECORD)
+  uint32_t* doff = nullptr;  // replay: CSR row offsets of `tape` (set_decisions)
   bool submitted = false;    // mr_batch_submit enqueued a step not yet finished
   std::chrono::steady_clock::time_point t_submit;
 };
@@ -242,7 +243,7 @@ static int validate(const mr_cfg* c) {
   return 0;
 }
 
-int mr_batch_create(const mr_cfg* cfg, mr_batch** out) {
+static int mr_batch_create_impl(const mr_cfg* cfg, mr_batch** out) {
   if (!out) return set_err("null out");
   *out = nullptr;
   if (validate(cfg) != 0) return -1;
@@ -509,7 +510,7 @@ int mr_batch_finish(mr_batch* b, mr_run_stats* st, mr_counters* cnt) {
   return 0;
 }
 
-int mr_batch_verdicts(mr_batch* b, uint16_t* code, uint32_t* time_us, uint64_t* digest) {
+static int mr_batch_verdicts_impl(mr_batch* b, uint16_t* code, uint32_t* time_us, uint64_t* digest) {
   if (!b) return set_err("null batch");
   HIPCHK(hipSetDevice(b->cfg.device));
   size_t C = b->D.C;
@@ -593,49 +594,79 @@ uint32_t mr_decision_word(uint32_t v, uint32_t lo, uint32_t hi) {
   return (uint32_t)((num + span - 1) / span);
 }
 
+// the batch's decision tables (replay rows + offsets, or the record tape) freed; Philox draws
+static void drop_decisions(mr_batch* b) {
+  if (b->tape) (void)hipFree(b->tape);
+  if (b->doff) (void)hipFree(b->doff);
+  b->tape = nullptr;
+  b->doff = nullptr;
+  b->D.dtab = nullptr; b->D.doff = nullptr; b->D.dcap = 0; b->D.tape_mode = 0;
+}
+
+// Keyed decisions as CSR rows: every decision once (16 B each) plus C + 1 offsets, so the
+// table is O(n + C) whatever the longest row. Everything is validated and staged before the
+// previous table is dropped, so a rejected call leaves the batch as it was.
+static int set_decisions_impl(mr_batch* b, const mr_decision* d, size_t n) {
+  const size_t C = b->D.C;
+  if (n >= (1ull << 32)) return set_err("too many decisions for one batch (2^32 - 1 at most)");
+  std::vector<uint32_t> off(C + 1, 0);
+  for (size_t i = 0; i < n; i++) {
+    if (d[i].cluster >= C) return set_err("decision for a cluster outside the batch");
+    if (d[i].stream < MR_DS_TESTER || d[i].stream > MR_DS_NET) return set_err("bad decision stream");
+    off[d[i].cluster + 1]++;
+  }
+  for (size_t c = 0; c < C; c++) off[c + 1] += off[c];
+  std::vector<uint4> tab(n);
+  std::vector<uint32_t> fill(off.begin(), off.end() - 1);
+  for (size_t i = 0; i < n; i++) {
+    const mr_decision& r = d[i];
+    tab[fill[r.cluster]++] = make_uint4(((uint32_t)r.stream << 16) | r.entity, r.seq, r.w0, r.w1);
+  }
+  auto lt = [](const uint4& a, const uint4& c) { return a.x < c.x || (a.x == c.x && a.y < c.y); };
+  for (size_t c = 0; c < C; c++) {
+    uint4* row = tab.data() + off[c];
+    const uint32_t cnt = off[c + 1] - off[c];
+    std::sort(row, row + cnt, lt);
+    for (uint32_t k = 1; k < cnt; k++)
+      if (row[k].x == row[k - 1].x && row[k].y == row[k - 1].y)
+        return set_err("duplicate decision key (cluster " + std::to_string(c) + ")");
+  }
+  uint4* dtab = nullptr;
+  uint32_t* doff = nullptr;
+  hipError_t e = hipMalloc(&dtab, (n ? n : 1) * sizeof(uint4));
+  if (e == hipSuccess) e = hipMalloc(&doff, off.size() * sizeof(uint32_t));
+  if (e == hipSuccess && n)
+    e = hipMemcpy(dtab, tab.data(), n * sizeof(uint4), hipMemcpyHostToDevice);
+  if (e == hipSuccess)
+    e = hipMemcpy(doff, off.data(), off.size() * sizeof(uint32_t), hipMemcpyHostToDevice);
+  if (e != hipSuccess) {
+    if (dtab) (void)hipFree(dtab);
+    if (doff) (void)hipFree(doff);
+    return set_err(std::string("decision table: ") + hipGetErrorString(e));
+  }
+  drop_decisions(b);
+  b->tape = dtab;
+  b->doff = doff;
+  b->D.dtab = dtab;
+  b->D.doff = doff;
+  b->D.tape_mode = 1;
+  return 0;
+}
+
 int mr_batch_set_decisions(mr_batch* b, const mr_decision* d, size_t n) {
   if (!b) return set_err("null batch");
   if (n && !d) return set_err("null decisions");
   HIPCHK(hipSetDevice(b->cfg.device));
   HIPCHK(hipStreamSynchronize(b->stream));
-  if (b->tape) { HIPCHK(hipFree(b->tape)); b->tape = nullptr; }
-  b->D.dtab = nullptr; b->D.dcap = 0; b->D.tape_mode = 0;
-  if (!n) return 0;
-  const size_t C = b->D.C;
-  std::vector<uint32_t> cnt(C, 0);
-  for (size_t i = 0; i < n; i++) {
-    if (d[i].cluster >= C) return set_err("decision for a cluster outside the batch");
-    if (d[i].stream < MR_DS_TESTER || d[i].stream > MR_DS_NET) return set_err("bad decision stream");
-    cnt[d[i].cluster]++;
+  if (!n) { drop_decisions(b); return 0; }
+  try {  // host staging may not fit: an error code across the C ABI, never an exception
+    return set_decisions_impl(b, d, n);
+  } catch (const std::bad_alloc&) {
+    return set_err("decision table: host allocation failed");
   }
-  uint32_t mx = 1;
-  for (uint32_t c : cnt) mx = c > mx ? c : mx;
-  uint32_t cap = 1;
-  while (cap < mx) cap <<= 1;
-  std::vector<uint4> tab((size_t)C * cap, make_uint4(~0u, ~0u, 0u, 0u));
-  std::vector<uint32_t> fill(C, 0);
-  for (size_t i = 0; i < n; i++) {
-    const mr_decision& r = d[i];
-    tab[(size_t)r.cluster * cap + fill[r.cluster]++] =
-        make_uint4(((uint32_t)r.stream << 16) | r.entity, r.seq, r.w0, r.w1);
-  }
-  auto lt = [](const uint4& a, const uint4& c) { return a.x < c.x || (a.x == c.x && a.y < c.y); };
-  for (size_t c = 0; c < C; c++) {
-    uint4* row = tab.data() + c * cap;
-    std::sort(row, row + cnt[c], lt);
-    for (uint32_t k = 1; k < cnt[c]; k++)
-      if (row[k].x == row[k - 1].x && row[k].y == row[k - 1].y)
-        return set_err("duplicate decision key (cluster " + std::to_string(c) + ")");
-  }
-  HIPCHK(hipMalloc(&b->tape, tab.size() * sizeof(uint4)));
-  HIPCHK(hipMemcpy(b->tape, tab.data(), tab.size() * sizeof(uint4), hipMemcpyHostToDevice));
-  b->D.dtab = b->tape;
-  b->D.dcap = cap;
-  b->D.tape_mode = 1;
-  return 0;
 }
 
-int mr_batch_get_decisions(mr_batch* b, uint32_t k, mr_decision* out, size_t cap, size_t* n) {
+static int mr_batch_get_decisions_impl(mr_batch* b, uint32_t k, mr_decision* out, size_t cap, size_t* n) {
   if (!b || !n) return set_err("null argument");
   if (k >= b->D.C) return set_err("cluster out of range");
   HIPCHK(hipSetDevice(b->cfg.device));
@@ -656,7 +687,7 @@ int mr_batch_get_decisions(mr_batch* b, uint32_t k, mr_decision* out, size_t cap
   return 0;
 }
 
-int mr_replay(const mr_cfg* cfg, const mr_decision* d, size_t n, mr_event* out, size_t cap,
+static int mr_replay_impl(const mr_cfg* cfg, const mr_decision* d, size_t n, mr_event* out, size_t cap,
               size_t* n_out, uint16_t* code, uint32_t* time_us, uint64_t* misses) {
   if (!cfg || !n_out) return set_err("null argument");
   if (n && !d) return set_err("null decisions");
@@ -706,6 +737,7 @@ void mr_batch_destroy(mr_batch* b) {
 #endif
   if (b->base) (void)hipFree(b->base);
   if (b->tape) (void)hipFree(b->tape);
+  if (b->doff) (void)hipFree(b->doff);
   if (b->red) (void)hipFree(b->red);
   if (b->h_remaining) (void)hipHostFree(b->h_remaining);
   if (b->h_ctl0) (void)hipHostFree(b->h_ctl0);
@@ -713,6 +745,39 @@ void mr_batch_destroy(mr_batch* b) {
   if (b->ev1) (void)hipEventDestroy(b->ev1);
   if (b->stream) (void)hipStreamDestroy(b->stream);
   delete b;
+}
+
+int mr_batch_create(const mr_cfg* cfg, mr_batch** out) {
+  try {  // host allocations: an error code across the C ABI, never an exception
+    return mr_batch_create_impl(cfg, out);
+  } catch (const std::exception& e) {
+    return set_err(std::string("mr_batch_create: ") + e.what());
+  }
+}
+
+int mr_batch_verdicts(mr_batch* b, uint16_t* code, uint32_t* time_us, uint64_t* digest) {
+  try {  // host allocations: an error code across the C ABI, never an exception
+    return mr_batch_verdicts_impl(b, code, time_us, digest);
+  } catch (const std::exception& e) {
+    return set_err(std::string("mr_batch_verdicts: ") + e.what());
+  }
+}
+
+int mr_batch_get_decisions(mr_batch* b, uint32_t k, mr_decision* out, size_t cap, size_t* n) {
+  try {  // host allocations: an error code across the C ABI, never an exception
+    return mr_batch_get_decisions_impl(b, k, out, cap, n);
+  } catch (const std::exception& e) {
+    return set_err(std::string("mr_batch_get_decisions: ") + e.what());
+  }
+}
+
+int mr_replay(const mr_cfg* cfg, const mr_decision* d, size_t n, mr_event* out, size_t cap,
+              size_t* n_out, uint16_t* code, uint32_t* time_us, uint64_t* misses) {
+  try {  // host allocations: an error code across the C ABI, never an exception
+    return mr_replay_impl(cfg, d, n, out, cap, n_out, code, time_us, misses);
+  } catch (const std::exception& e) {
+    return set_err(std::string("mr_replay: ") + e.what());
+  }
 }
 
 }  // extern "C"

@@ -62,6 +62,17 @@ def lib():
     return L
 
 
+def lib_sha16(path=None):
+    """First 16 hex digits of the SHA-256 of the product library file (the build a
+    measurement was taken with: bench.py's JSON line and profiles/pmc_*.json carry it)."""
+    import hashlib
+    h = hashlib.sha256()
+    with open(path or LIB_PATH, "rb") as f:
+        for blk in iter(lambda: f.read(1 << 20), b""):
+            h.update(blk)
+    return h.hexdigest()[:16]
+
+
 class SimError(RuntimeError):
     pass
 

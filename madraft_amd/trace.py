@@ -33,8 +33,12 @@ def _range_value(w, lo, hi):
     return lo + ((int(w) * (hi - lo)) >> 32)
 
 
-def decisions_from_events(events, elect_lo_us=150_000, elect_hi_us=300_000):
-    """DECISION_DTYPE records for an iterable of event dicts (see the module docstring)."""
+def decisions_from_events(events, elect_lo_us=150_000, elect_hi_us=300_000, unreliable=None):
+    """DECISION_DTYPE records for an iterable of event dicts (see the module docstring).
+
+    A decoded send needs its network mode: the line's `"unreliable"`, else the `unreliable`
+    argument (the run's mode, e.g. the scenario's); with neither it is rejected, never guessed.
+    A dropped send (unreliable mode only: the reliable net loses nothing) needs no latency."""
     rows = []
     for e in events:
         kind, c = e["event"], int(e.get("cluster", 0))
@@ -44,8 +48,15 @@ def decisions_from_events(events, elect_lo_us=150_000, elect_hi_us=300_000):
             if raw:
                 w0, w1 = int(e["w0"]), int(e.get("w1", 0))
             else:
-                w0, w1 = _abi.net_decision(bool(e.get("dropped", False)), int(e["latency_us"]),
-                                           bool(e.get("unreliable", True)))
+                mode = e.get("unreliable", unreliable)
+                if mode is None:
+                    raise ValueError(f"send event without its network mode ('unreliable'): {e}")
+                dropped = bool(e.get("dropped", False))
+                if dropped and not mode:
+                    raise ValueError(f"dropped send in reliable mode (loss 0, tester.rs:127-137): {e}")
+                if not dropped and "latency_us" not in e:
+                    raise ValueError(f"delivered send without latency_us: {e}")
+                w0, w1 = _abi.net_decision(dropped, int(e.get("latency_us", LAT_LO)), bool(mode))
         elif kind == "election_timeout":
             stream, ent = _abi.MR_DS_ELECT, int(e["node"])
             w0 = int(e["w0"]) if raw else _abi.decision_word(int(e["timeout_us"]), elect_lo_us,
@@ -100,7 +111,7 @@ def events_from_decisions(d, unreliable=True, elect_lo_us=150_000, elect_hi_us=3
     return out
 
 
-def load_jsonl(path, **kw):
+def load_jsonl(path, **kw):  # kw: decisions_from_events' (elect_lo_us, elect_hi_us, unreliable)
     """decisions_from_events over a JSON-lines file (blank lines and # comments skipped)."""
     with open(path) as f:
         ev = [json.loads(line) for line in f if line.strip() and not line.lstrip().startswith("#")]

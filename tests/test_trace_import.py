@@ -10,7 +10,7 @@ import json
 import numpy as np
 import pytest
 
-from madraft_amd import trace
+from madraft_amd import _abi, trace
 
 CAP = 1 << 15
 
@@ -86,6 +86,26 @@ def test_bad_events_are_rejected():
         trace.decisions_from_events([{"event": "crash", "node": 1, "index": 0}])
     with pytest.raises(ValueError):
         trace.decisions_from_events([{"event": "rng", "thread": 70000, "index": 0, "u64": 1}])
+    # a decoded send needs its network mode (the line's or the caller's), never a guessed one
+    with pytest.raises(ValueError):
+        trace.decisions_from_events([{"event": "send", "host": 0, "index": 0, "latency_us": 2000}])
+    with pytest.raises(ValueError):  # the reliable net loses nothing (tester.rs:127-137)
+        trace.decisions_from_events([{"event": "send", "host": 0, "index": 0, "dropped": True,
+                                      "unreliable": False}])
+    with pytest.raises(ValueError):
+        trace.decisions_from_events([{"event": "send", "host": 0, "index": 0, "unreliable": True}])
+
+
+def test_send_mode_and_dropped_defaults():
+    rel = trace.decisions_from_events([{"event": "send", "host": 1, "index": 2, "latency_us": 9000}],
+                                      unreliable=False)
+    unr = trace.decisions_from_events([{"event": "send", "host": 1, "index": 2, "latency_us": 9000}],
+                                      unreliable=True)
+    assert int(rel["w1"][0]) != int(unr["w1"][0])  # the latency word depends on the mode
+    assert trace.events_from_decisions(rel, unreliable=False)[0]["latency_us"] == 9000
+    dropped = trace.decisions_from_events([{"event": "send", "host": 1, "index": 2, "dropped": True,
+                                            "unreliable": True}])
+    assert int(dropped["w0"][0]) < _abi.LOSS_Q32
 
 
 @pytest.mark.gpu
