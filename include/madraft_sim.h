@@ -93,6 +93,10 @@ enum mr_scenario {
   MR_SCN_KV_SNAPSHOT_UNRELIABLE_3B = 43,           /* kvraft/tests.rs:506-510 */
   MR_SCN_KV_SNAPSHOT_UNRELIABLE_RECOVER_3B = 44,   /* kvraft/tests.rs:512-516 */
   MR_SCN_KV_SNAPSHOT_UNRELIABLE_RECOVER_CONCURRENT_PARTITION_3B = 45, /* kvraft/tests.rs:518-522 */
+  /* generic_test_linearizability (15 clients, 7 servers): the reference's commented-out
+   * kvraft/tests.rs:386-390 and 524-528, defined by the build (docs/SEMANTICS.md §9b) */
+  MR_SCN_KV_PERSIST_PARTITION_UNRELIABLE_LINEARIZABLE_3A = 46,
+  MR_SCN_KV_SNAPSHOT_UNRELIABLE_RECOVER_CONCURRENT_PARTITION_LINEARIZABLE_3B = 47,
   MR_SCN_COUNT_
 };
 
@@ -100,9 +104,16 @@ enum mr_scenario {
 static inline int mr_scn_is_kv(uint32_t s) {
   return (s >= MR_SCN_KV_BASIC_3A && s <= MR_SCN_KV_UNRELIABLE_3A) ||
          (s >= MR_SCN_KV_MANY_PARTITIONS_ONE_CLIENT_3A &&
-          s <= MR_SCN_KV_SNAPSHOT_UNRELIABLE_RECOVER_CONCURRENT_PARTITION_3B);
+          s <= MR_SCN_KV_SNAPSHOT_UNRELIABLE_RECOVER_CONCURRENT_PARTITION_LINEARIZABLE_3B);
 }
 /* default log / apply capacity of a kvraft scenario (no snapshots: every op stays in the log) */
+/* generic_test_linearizability scenarios (SEMANTICS §9b) */
+static inline int mr_scn_is_lin15(uint32_t s) {
+  return s == MR_SCN_KV_PERSIST_PARTITION_UNRELIABLE_LINEARIZABLE_3A ||
+         s == MR_SCN_KV_SNAPSHOT_UNRELIABLE_RECOVER_CONCURRENT_PARTITION_LINEARIZABLE_3B;
+}
+/* scenarios whose clerks keep more than 64 messages in flight: 256 message slots */
+static inline int mr_scn_wide_slots(uint32_t s) { return s == MR_SCN_KV_SNAPSHOT_RECOVER_MANY_CLIENTS_3B; }
 static inline uint32_t mr_kv_log_cap(uint32_t s) {
   if (s == MR_SCN_KV_SNAPSHOT_RECOVER_MANY_CLIENTS_3B) return 16384u;
   return (s == MR_SCN_KV_BASIC_3A || s == MR_SCN_KV_UNRELIABLE_3A || s >= MR_SCN_KV_UNRELIABLE_ONE_KEY_3A ||
@@ -219,7 +230,11 @@ typedef struct mr_cfg {
                            * waves / SIMD x SIMDs x 64). A bigger batch runs as consecutive
                            * chunks of `lanes` clusters (or streams them, MR_F_STREAM) instead of
                            * queueing waves behind the resident ones. Results do not depend on it. */
-  uint32_t reserved[4];
+  uint32_t lanes_per_wave;/* lanes of each 64-lane wave that hold a cluster: 64, 32 or 16 (0 = auto:
+                           * 32 when the batch fills at most half the resident lanes, so a small
+                           * batch still runs two waves per SIMD; else 64). Results do not depend
+                           * on it. */
+  uint32_t reserved[3];
 } mr_cfg;
 
 /* Whole-batch counters (sums over clusters unless named max/first). */

@@ -42,6 +42,9 @@ SCENARIOS = [
     "snapshot_rpc_3b", "snapshot_size_3b", "snapshot_recover_3b", "snapshot_recover_many_clients_3b",
     "snapshot_unreliable_3b", "snapshot_unreliable_recover_3b",
     "snapshot_unreliable_recover_concurrent_partition_3b",
+    # generic_test_linearizability (15 clients, 7 servers; SEMANTICS §9b)
+    "persist_partition_unreliable_linearizable_3a",
+    "snapshot_unreliable_recover_concurrent_partition_linearizable_3b",
 ]
 SCENARIO_ID = {n: i for i, n in enumerate(SCENARIOS) if n}
 # tests that still need multi-threaded tester programs (spawn_local); not built yet
@@ -53,7 +56,10 @@ KV_TESTS = ["basic_3a", "concurrent_3a", "unreliable_3a", "many_partitions_one_c
             "persist_partition_unreliable_3a", "unreliable_one_key_3a", "one_partition_3a",
             "snapshot_rpc_3b", "snapshot_size_3b", "snapshot_recover_3b",
             "snapshot_recover_many_clients_3b", "snapshot_unreliable_3b",
-            "snapshot_unreliable_recover_3b", "snapshot_unreliable_recover_concurrent_partition_3b"]
+            "snapshot_unreliable_recover_3b", "snapshot_unreliable_recover_concurrent_partition_3b",
+            "persist_partition_unreliable_linearizable_3a",
+            "snapshot_unreliable_recover_concurrent_partition_linearizable_3b"]
+LIN_TESTS = KV_TESTS[-2:]  # generic_test_linearizability (SEMANTICS §9b)
 GPU_UNSUPPORTED = set(UNSUPPORTED)
 
 FAIL_NAMES = {
@@ -85,7 +91,7 @@ class MrCfg(C.Structure):
         ("hb_us", C.c_uint32), ("elect_lo_us", C.c_uint32), ("elect_hi_us", C.c_uint32),
         ("max_events", C.c_uint32), ("trace_clusters", C.c_uint32), ("trace_cap", C.c_uint32),
         ("device", C.c_int32), ("tape_cap", C.c_uint32), ("lanes", C.c_uint32),
-        ("reserved", C.c_uint32 * 4),
+        ("lanes_per_wave", C.c_uint32), ("reserved", C.c_uint32 * 3),
     ]
 
 

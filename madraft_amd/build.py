@@ -24,7 +24,7 @@ def _stale(out, srcs):
 
 # step-kernel instances (one per scenario id, mr_dev.h MR_ALL_SCNS) are split
 # over several translation units of mr_kernel.hip compiled in parallel
-SCN_IDS = list(range(1, 46))
+SCN_IDS = list(range(1, 48))
 N_GROUPS = 8
 # scenarios whose kernels carry 256 message slots (snapshot_recover_many_clients_3b: up to
 # 229 messages in flight with 20 clerks)
@@ -35,7 +35,7 @@ WIDE_SLOTS = {42}
 NB7_SCNS = {19, 20, 21, 22, 23}
 # the scenarios' default server counts (mr_dev.h k_default_n): each scenario
 # gets an instance sized for it (NB = 3 or 5) and one for up to 8 servers
-DEFAULT_N = [0, 3, 3, 7, 5, 3, 5, 3, 3, 5, 3, 3, 5, 3, 5, 5, 5, 5, 5, 3, 3, 3, 3, 3, 5, 5, 5, 5, 3, 3, 5, 5, 5, 5, 5, 5, 5, 3, 5, 3, 3, 5, 5, 5, 5, 5]
+DEFAULT_N = [0, 3, 3, 7, 5, 3, 5, 3, 3, 5, 3, 3, 5, 3, 5, 5, 5, 5, 5, 3, 3, 3, 3, 3, 5, 5, 5, 5, 3, 3, 5, 5, 5, 5, 5, 5, 5, 3, 5, 3, 3, 5, 5, 5, 5, 5, 7, 7]
 
 
 def _units(csrc, scns=None):

@@ -107,6 +107,8 @@ enum : uint32_t {
   KT_MCL,            // 1 = a clerk of the test body in a slot that is not a thread
   KT_LLO,            // a Get's linearizability lower bound at its call (SEMANTICS §9a)
   KT_TOP, KT_TKEY, KT_TELEM, KT_TCNT,  // a task's call: op, key, elem (or appender), calls
+  KT_LEP, KT_LNP,    // generic_test_linearizability (§9b): the key's Put epoch at the call, no
+                     // Put pending at the call
   KT__N
 };
 constexpr uint32_t KT_W = KT_ID;
@@ -134,6 +136,11 @@ constexpr uint32_t KV_SNAP_EVERY = 16;
 // linearizability bookkeeping per (key, appender): tag (cli + 1), appends called, appends
 // acknowledged, largest count a returned Get observed, an all-appenders Get's lower bound
 constexpr uint32_t LINW = 8;
+// generic_test_linearizability (SEMANTICS §9b): 15 clients share keys 0..14, each key record
+// is 32 words (hash lo, hi, length, the states of clients 0..14 by id: count | last j << 12 |
+// bad << 31), and the tester keeps per key 32 words of lin32: called[15], acked[15], the Put
+// epoch and the Puts pending; word 512 + cli of the cluster's lin32: client cli's next j
+constexpr uint32_t LIN_CLI = 15, KV_KW15 = 32, LIN15_J = 512;
 // ---- shard_ctrler (SEMANTICS §10): per-server append-only config store and a
 // per-cluster table of clerk operations (the log command names an operation)
 constexpr uint32_t N_SHARDS = 10;  // shard_ctrler/mod.rs:9
@@ -184,9 +191,11 @@ struct Dev {
   uint32_t nthr;    // thread slots of kt32 (0 = none)
   mr_event* trace;  // [trace_clusters][trace_cap]
   uint32_t* led;    // [C][LED_W] MR_F_SAFETY: bit t = a leader was elected in term t
-  uint32_t* lin32;  // [C][KV_KEYS][KV_APP][LINW] kvraft linearizability bookkeeping (§9a)
+  uint32_t* lin32;  // [C][KV_KEYS][KV_APP][LINW] kvraft linearizability bookkeeping (§9a, §9b)
+  uint32_t lin15;   // generic_test_linearizability layout (§9b): key records / bookkeeping
   uint32_t* remaining;  // [2]: clusters without verdict after a step launch; next unclaimed cluster
-  uint32_t L;           // lanes per launch: lane l starts with cluster c0 + l (chunk [c0, c0 + L))
+  uint32_t L;           // clusters per launch: lane l starts with cluster c0 + l (chunk [c0, c0 + L))
+  uint32_t lpw;         // lanes of each 64-lane block that hold a cluster (64, 32, 16; the rest idle)
   uint32_t c0;          // first cluster of this launch's chunk
   uint32_t stream;      // MR_F_STREAM: a lane that finishes takes the next unclaimed cluster
   unsigned long long* prof;  // [PROF_SLOTS] wave-cycle profile (MR_PROF builds only)
@@ -199,11 +208,11 @@ constexpr uint32_t LED_W = 64, LED_TERMS = 32 * LED_W;
 constexpr bool is_kv(uint32_t s) {
   return (s >= MR_SCN_KV_BASIC_3A && s <= MR_SCN_KV_UNRELIABLE_3A) ||
          (s >= MR_SCN_KV_MANY_PARTITIONS_ONE_CLIENT_3A &&
-          s <= MR_SCN_KV_SNAPSHOT_UNRELIABLE_RECOVER_CONCURRENT_PARTITION_3B);
+          s <= MR_SCN_KV_SNAPSHOT_UNRELIABLE_RECOVER_CONCURRENT_PARTITION_LINEARIZABLE_3B);
 }
 // generic_test(nclients, unreliable, crash, partitions, maxraftstate) of a kvraft scenario
 // (kvraft/tests.rs:222-384, 494-522); snapshot_rpc / snapshot_size use maxraftstate too
-struct KvGen { uint32_t nc; bool unrel, crash, part; uint32_t maxraft; };
+struct KvGen { uint32_t nc; bool unrel, crash, part; uint32_t maxraft; bool lin; };
 constexpr KvGen kv_gen(uint32_t s) {
   switch (s) {
     case MR_SCN_KV_BASIC_3A: return {1, false, false, false};
@@ -225,7 +234,11 @@ constexpr KvGen kv_gen(uint32_t s) {
     case MR_SCN_KV_SNAPSHOT_UNRELIABLE_3B: return {5, true, false, false, 1000};
     case MR_SCN_KV_SNAPSHOT_UNRELIABLE_RECOVER_3B: return {5, true, true, false, 1000};
     case MR_SCN_KV_SNAPSHOT_UNRELIABLE_RECOVER_CONCURRENT_PARTITION_3B: return {5, true, true, true, 1000};
-    default: return {0, false, false, false, 0};
+    // generic_test_linearizability (15 clients, 7 servers; SEMANTICS §9b)
+    case MR_SCN_KV_PERSIST_PARTITION_UNRELIABLE_LINEARIZABLE_3A: return {15, true, true, true, 0, true};
+    case MR_SCN_KV_SNAPSHOT_UNRELIABLE_RECOVER_CONCURRENT_PARTITION_LINEARIZABLE_3B:
+      return {15, true, true, true, 1000, true};
+    default: return {0, false, false, false, 0, false};
   }
 }
 constexpr bool is_ctrl(uint32_t s) { return s == MR_SCN_CTRL_BASIC_4A || s == MR_SCN_CTRL_MULTI_4A; }
@@ -255,7 +268,7 @@ template <uint32_t S, uint32_t NB>
 hipError_t launch_step_tape_t(const Dev& D, uint32_t budget, hipStream_t s);
 constexpr uint8_t k_default_n[] = {0, 3, 3, 7, 5, 3, 5, 3, 3, 5, 3, 3, 5, 3, 5,
                                    5, 5, 5, 5, 3, 3, 3, 3, 3, 5, 5, 5, 5, 3, 3,
-                                   5, 5, 5, 5, 5, 5, 5, 3, 5, 3, 3, 5, 5, 5, 5, 5};
+                                   5, 5, 5, 5, 5, 5, 5, 3, 5, 3, 3, 5, 5, 5, 5, 5, 7, 7};
 constexpr uint32_t nb_of(uint32_t s) { return k_default_n[s] <= 5 ? k_default_n[s] : 8u; }
 // scenarios with a 7-server instance as well (BASELINE config 4 runs the 2D tests with 7
 // servers; arrays sized for 7 keep fewer registers live than the 8-server instance)
@@ -275,6 +288,6 @@ constexpr bool uses_service_snapshots(uint32_t s) {
   MR_INST(26) MR_INST(27) MR_INST(15) MR_INST(17) MR_INST(18) MR_INST(28) MR_INST(29)     \
   MR_INST(30) MR_INST(31) MR_INST(32) MR_INST(33) MR_INST(34) MR_INST(35) MR_INST(36)     \
   MR_INST(37) MR_INST(38) MR_INST(39) MR_INST(40) MR_INST(41) MR_INST(42) MR_INST(43)     \
-  MR_INST(44) MR_INST(45)
+  MR_INST(44) MR_INST(45) MR_INST(46) MR_INST(47)
 
 }  // namespace mr

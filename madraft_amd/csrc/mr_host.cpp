@@ -88,13 +88,16 @@ const char* k_names[MR_SCN_COUNT_] = {
     "persist_partition_unreliable_3a", "unreliable_one_key_3a", "one_partition_3a",
     "snapshot_rpc_3b", "snapshot_size_3b", "snapshot_recover_3b", "snapshot_recover_many_clients_3b",
     "snapshot_unreliable_3b", "snapshot_unreliable_recover_3b",
-    "snapshot_unreliable_recover_concurrent_partition_3b"};
+    "snapshot_unreliable_recover_concurrent_partition_3b",
+    "persist_partition_unreliable_linearizable_3a",
+    "snapshot_unreliable_recover_concurrent_partition_linearizable_3b"};
 // servers per test (tests.rs `let servers = ..`)
 const uint8_t k_nodes[MR_SCN_COUNT_] = {0, 3, 3, 7, 5, 3, 5, 3, 3, 5, 3, 3, 5, 3,
                                         5, 5, 5, 5, 5, 3, 3, 3, 3, 3, 5, 5, 5, 5, 3, 3,
-                                        5, 5, 5, 5, 5, 5, 5, 3, 5, 3, 3, 5, 5, 5, 5, 5};
+                                        5, 5, 5, 5, 5, 5, 5, 3, 5, 3, 3, 5, 5, 5, 5, 5, 7, 7};
 
 constexpr size_t RED_N = CNT__N + 8 + 64 + 32 + 3;  // reduce_kernel output slots
+constexpr uint32_t STEP_LANES = 64;  // lanes per step-kernel block (one wave)
 }  // namespace
 
 struct mr_batch {
@@ -212,7 +215,7 @@ int mr_cfg_init(mr_cfg* c, uint32_t scn) {
   c->apply_cap = cap ? cap : (snap ? 1024 : 512);
   /* in-flight maxima over 64K / 1K seeds: 20 (figure_8), <= 45 (7 / 8 servers,
    * kvraft), 229 (20 clerks); a send past msg_slots fails the cluster (MR_FAIL_SIM_CAPACITY) */
-  c->msg_slots = scn == MR_SCN_KV_SNAPSHOT_RECOVER_MANY_CLIENTS_3B ? 256 : kv ? 64 : 32;
+  c->msg_slots = mr_scn_wide_slots(scn) ? 256 : kv ? 64 : 32;
   c->ae_max = 16;
   c->hb_us = 50000;
   c->elect_lo_us = 150000;  // raft.rs:262
@@ -231,13 +234,16 @@ static int validate(const mr_cfg* c) {
   if (c->log_cap < 16 || (c->log_cap & (c->log_cap - 1))) return set_err("log_cap: power of 2 >= 16");
   if (c->apply_cap < 16) return set_err("apply_cap too small");
   if (c->msg_slots < 1 || c->msg_slots > MR_MAX_MSG_SLOTS ||
-      (c->msg_slots > 64 && c->scenario != MR_SCN_KV_SNAPSHOT_RECOVER_MANY_CLIENTS_3B))
+      (c->msg_slots > 64 && !mr_scn_wide_slots(c->scenario)))
     return set_err("msg_slots must be 1..64 (1..256 for snapshot_recover_many_clients_3b)");
   if (c->ae_max < 1 || c->ae_max > MR_MAX_AE) return set_err("ae_max must be 1..32");
   if (c->elect_hi_us <= c->elect_lo_us || c->hb_us == 0) return set_err("bad timers");
   if (c->max_events == 0) return set_err("max_events must be > 0");
   if ((c->flags & MR_F_TRACE) && (c->trace_cap == 0 || c->trace_clusters > c->n_clusters))
     return set_err("bad trace config");
+  if (c->lanes_per_wave != 0 && c->lanes_per_wave != 16 && c->lanes_per_wave != 32 &&
+      c->lanes_per_wave != 64)
+    return set_err("lanes_per_wave must be 0 (auto), 16, 32 or 64");
   if ((c->flags & MR_F_RECORD) && c->tape_cap < 1)
     return set_err("MR_F_RECORD needs tape_cap >= 1 (decisions kept per cluster)");
   return 0;
@@ -266,6 +272,7 @@ static int mr_batch_create_impl(const mr_cfg* cfg, mr_batch** out) {
   D.bugs = cfg->flags & (MR_F_BUG_VOTE_TWICE | MR_F_BUG_VOTE_STALE | MR_F_BUG_NO_PREV_CHECK |
                          MR_F_BUG_NO_DEDUP | MR_F_BUG_STALE_READ);
   D.links = kv_gen(cfg->scenario).part ? 1u : 0u;  // server-link cuts (CS_CUT) can exist
+  D.lin15 = mr_scn_is_lin15(scn) ? 1u : 0u;  // generic_test_linearizability layout (SEMANTICS §9b)
   D.trace_clusters = (cfg->flags & MR_F_TRACE) ? cfg->trace_clusters : 0u;
   D.trace_cap = cfg->trace_cap;
   D.scenario = scn;
@@ -354,9 +361,15 @@ static int mr_batch_create_impl(const mr_cfg* cfg, mr_batch** out) {
     mr_batch_destroy(b);
     return set_err("hipMemset failed");
   }
+  // lanes per wave: as configured, else 32 when the batch (or its chunk) fills at most half of
+  // the resident lanes — two half-full waves per SIMD hide the latency chains better than one
+  // full one — else 64
+  const uint32_t cap = step_capacity(b->D, scn, cfg->device);  // resident lanes (64 per wave)
+  b->D.lpw = cfg->lanes_per_wave ? cfg->lanes_per_wave
+             : (cap && (uint64_t)(cfg->lanes && cfg->lanes < C ? cfg->lanes : C) * 2u <= cap) ? 32u : 64u;
   if (!cfg->lanes) {  // a batch bigger than the resident waves runs as chunks of that size
-    const uint32_t cap = step_capacity(b->D, scn, cfg->device);
-    if (cap && cap < b->D.C) b->D.L = cap;
+    const uint32_t capc = (uint32_t)((uint64_t)cap * b->D.lpw / STEP_LANES);
+    if (capc && capc < b->D.C) b->D.L = capc;
   }
   if (const char* s = std::getenv("MR_STEP_BUDGET")) b->budget = (uint32_t)std::atoi(s);
   if (b->budget == 0) b->budget = 16384;

@@ -130,7 +130,7 @@ extern __shared__ uint64_t s_keys_raw[];
 enum : uint32_t {
   P_TAIL, P_SEL, P_DECODE, P_LOAD, P_DROP, P_RVREQ, P_RVREP, P_AEREQ, P_AEREP, P_ISREQ, P_ISREP,
   P_HB, P_ELECT, P_APPLY, P_SEND, P_STORE, P_TESTER, P_STEPDOWN, P_PRO, P_EPI,
-  P_S_SETUP, P_S_NET, P_S_PAY, P_AE_PROBE, P_AP_LOAD, P_AP_CHECK, P_DRAW, P__N
+  P_S_SETUP, P_S_NET, P_S_PAY, P_AE_PROBE, P_AP_LOAD, P_AP_CHECK, P__N
 };
 #ifdef MR_PROF
 __shared__ unsigned long long s_prof[STEP_BLOCK / 64][2 * P__N + 1];
@@ -364,7 +364,9 @@ __device__ __forceinline__ uint64_t fnv8(uint64_t h, uint32_t w0, uint32_t w1, u
 }
 DI void rec8(const Dev& D, X& x, uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3, uint32_t w4,
              uint32_t w5, uint32_t w6, uint32_t w7) {
+#ifndef MR_DEV_NO_DIGEST  // timing experiments only: NOT the simulator (breaks the digest)
   x.digest = fnv8(x.digest, w0, w1, w2, w3, w4, w5, w6, w7);
+#endif
   if (x.c < D.trace_clusters && x.trace_n < D.trace_cap) {
     uint32_t* p = reinterpret_cast<uint32_t*>(D.trace + (size_t)x.c * D.trace_cap + x.trace_n);
     p[0] = w0; p[1] = w1; p[2] = w2; p[3] = w3; p[4] = w4; p[5] = w5; p[6] = w6; p[7] = w7;
@@ -857,16 +859,14 @@ DI void node_apply(const Dev& D, X& x, uint32_t me, NC& d, bool& kvready) {
 #define MR_AP_COOP 1
 #endif
 template <uint32_t S>
-DI void node_apply_coop(const Dev& D, X& x, uint32_t me, NC& d, bool owner) {
+DI void node_apply_coop(const Dev& D, X& x, uint32_t me, NC& d) {
   // snap_common (the 2D tests, uses_service_snapshots) runs with service snapshots:
   // t_new(snapshot = true) precedes every node event of such a batch, so the mode is the same
   // for every lane here. A scenario whose runtime mode (x.netmode bit 1, what node_apply
   // reads) disagrees would skip or invent snapshots: it fails loudly instead.
   constexpr bool snapmode = uses_service_snapshots(S);
-  if (owner && ((x.netmode >> 1) & 1u) != (snapmode ? 1u : 0u)) { fail(D, x, MR_FAIL_SIM_BAD_PROGRAM); owner = false; }
-  // owners: lanes whose node event has committed entries to apply; every other lane of the
-  // call (events without entries, lanes waiting this iteration) only helps
-  const uint32_t cnt = owner && d.commit > d.applied ? d.commit - d.applied : 0u;
+  if (((x.netmode >> 1) & 1u) != (snapmode ? 1u : 0u)) { fail(D, x, MR_FAIL_SIM_BAD_PROGRAM); return; }
+  const uint32_t cnt = d.commit > d.applied ? d.commit - d.applied : 0u;
   const uint32_t base = d.applied + 1u, len0 = d.slen;
   // per-owner LDS words (the send-loop staging, unused until the send loop): first failure
   // key, last snapshot's term
@@ -1069,177 +1069,12 @@ DI void ae_load_batch(const Dev& D, const X& x, uint32_t me, const NC& d, uint32
   }
 }
 
-// A node event's state between its phases (node_event_a -> the wave-uniform section ->
-// node_event_c), in registers: the node's scalars and peers, what the handler decided to send.
-struct NE {
-  NC d;
-  PV pv;
-  uint2 prange;  // the pending payload range as loaded with the record (MR_PLO_EARLY)
-  uint32_t me, src, inc, seq, kind, mode, peers, rtype, ra, rb, nrst, reach;
-  uint32_t rawt[NB];
-  bool kvready, is_msg;
-};
-
-// Cooperative draws. A draw is a pure function of its key (SEMANTICS §2: counter (seq, entity,
-// stream), key the cluster's seed), so any lane can compute any lane's draw. After the
-// handlers, every lane of the wave — the ones with a node event and the ones waiting — takes
-// one item of the wave's pending draws per round: each event's election-timer draw (its
-// nrst-th reset, the only one that reaches the timer) and the NET draws of its sends to
-// reachable peers, in peer order. Each draw is reduced to what its owner reads (the timer's
-// offset; a send's loss bit and latency) and written to the owner's send-staging words in LDS.
-// Before, a wave ran one Philox per timer reset and one per send-loop round, so up to five
-// per node iteration whatever the lanes' counts; now ceil(items / 64), mostly one.
-// MR_TAPE builds record / replay every draw in the event's own order: they keep the inline
-// draws, as do the 7 / 8-server kernels (their staging words are all in use).
-#ifndef MR_COOP_DRAW
-#define MR_COOP_DRAW 1
-#endif
-constexpr bool COOP_DRAW = MR_COOP_DRAW && !MR_TAPE && NB <= 5;
-constexpr uint32_t DRAW_J = 1 + (NB - 1);  // items per event: the timer + one per peer
-// result j of a lane: send-staging word 5, 6, 7, 13, 14 (LNX(p) uses 0..4, LPT(p) 8..12 at
-// NB <= 5; the cooperative applier's exchange words are 0 and 1)
-DI uint32_t res_word(uint32_t j) { return j < 3u ? 5u + j : 10u + j; }
-#define LRES(j) reinterpret_cast<uint32_t*>(s_keys + D.M * STEP_BLOCK)[res_word(j) * STEP_BLOCK + threadIdx.x]
-constexpr uint32_t DRAW_LOST = 0x80000000u;  // a send draw's loss bit (else the latency in us)
-
-// position of the k-th set bit (k < popcount) of a 64-bit mask
-DI uint32_t nth_bit64(uint64_t m, uint32_t k) {
-  uint32_t pos = 0;
-  uint32_t c = (uint32_t)__builtin_popcount((uint32_t)m);
-  if (k >= c) { k -= c; pos = 32; m >>= 32; }
-#pragma unroll
-  for (uint32_t w = 16; w; w >>= 1) {
-    c = (uint32_t)__builtin_popcount((uint32_t)m & ((1u << w) - 1u));
-    if (k >= c) { k -= c; pos += w; m >>= w; }
-  }
-  return pos;
-}
-DI uint32_t nth_bit8(uint32_t m, uint32_t k) {
-  uint32_t pos = 0;
-#pragma unroll
-  for (uint32_t q = 0; q < 8; q++) {
-    const bool hit = bit(m, q) && k == 0u;
-    pos = hit ? q : pos;
-    k -= bit(m, q) && k != 0u ? 1u : 0u;
-    if (hit) k = ~0u;
-  }
-  return pos;
-}
-
-// the owner side: `cnt` items (0 for lanes without an event); wme = me | unreliable << 5 |
-// has_timer << 6 | reachable-send mask << 8 | all-send mask << 16; ctr0 / ectr: the counters
-// of the event's first send and of its timer draw
-DI void coop_draws(const Dev& D, const X& x, uint32_t cnt, uint32_t wme, uint32_t ctr0,
-                   uint32_t ectr) {
-  uint64_t lay[DRAW_J];
-  uint32_t off[DRAW_J + 1];
-  off[0] = 0;
-#pragma unroll
-  for (uint32_t j = 0; j < DRAW_J; j++) {
-    lay[j] = __ballot(cnt > j);
-    off[j + 1] = off[j] + (uint32_t)__popcll(lay[j]);
-  }
-  const uint32_t total = off[DRAW_J];
-  if (total == 0) return;
-  uint32_t* const stg = reinterpret_cast<uint32_t*>(s_keys + D.M * STEP_BLOCK);
-  const uint32_t lane = __lane_id(), wave0 = threadIdx.x - lane;
-  for (uint32_t w0 = 0; w0 < total; w0 += 64u) {  // wave-uniform rounds
-    const uint32_t w = w0 + lane;
-    // its layer j (layers nest: an empty one has only empty ones above it) and owner o
-    uint32_t j = 0, joff = 0;
-    uint64_t m = lay[0];
-#pragma unroll
-    for (uint32_t q = 1; q < DRAW_J; q++)
-      if (w >= off[q]) { j = q; m = lay[q]; joff = off[q]; }
-    const bool mine = w < total;
-    const uint32_t o = mine ? nth_bit64(m, w - joff) : lane;
-    const uint32_t oc = (uint32_t)__shfl((int)x.c, (int)o), ow = (uint32_t)__shfl((int)wme, (int)o);
-    const uint32_t oct = (uint32_t)__shfl((int)ctr0, (int)o), oe = (uint32_t)__shfl((int)ectr, (int)o);
-    if (mine) {
-      const uint32_t ht = (ow >> 6) & 1u, ent = ow & 31u;
-      const bool timer = ht && j == 0u;
-      uint32_t c0 = oe, st = ST_ELECT;
-      if (!timer) {
-        const uint32_t p = nth_bit8((ow >> 8) & 255u, j - ht);
-        c0 = oct + (uint32_t)__builtin_popcount(((ow >> 16) & 255u) & ((1u << p) - 1u));
-        st = ST_NET;
-      }
-      const uint64_t seed = D.seed0 + oc;
-      const uint2 r = philox2(c0, ent, st, (uint32_t)seed, (uint32_t)(seed >> 32));
-      const bool unrel = (ow >> 5) & 1u;
-      const uint32_t out = timer ? u_range(r.x, D.elo, D.ehi)
-                           : (r.x < (unrel ? LOSS_Q32 : 0u)) ? DRAW_LOST
-                                                              : u_range(r.y, 1000u, unrel ? 27000u : 10000u);
-      stg[res_word(j) * STEP_BLOCK + wave0 + o] = out;
-    }
-  }
-  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");  // results visible to their owners
-  __builtin_amdgcn_wave_barrier();
-}
-
-// madsim net send whose NET draw was taken cooperatively (coop_draws): `draw` = DRAW_LOST or
-// the latency in us. Everything else as net_send (the clog check first: a clogged send does
-// not use its draw).
-DI int net_send_drawn(const Dev& D, X& x, uint32_t src, uint32_t& nctr, uint32_t dst,
-                      uint32_t type, uint32_t inc, uint32_t term, uint32_t a, uint32_t b,
-                      uint32_t c, uint64_t v, uint32_t k, uint32_t draw) {
-  uint32_t seq = x.msgs_sent++;
-  nctr++;
-  if (!bit(x.conn, src) || !bit(x.conn, dst) || link_cut(D, x, src, dst)) {
-    CADD(CNT_DROP_CLOG, 1u);
-    return -1;
-  }
-  if (draw == DRAW_LOST) { CADD(CNT_DROP_LOSS, 1u); return -1; }
-  if (x.inflight >= D.M) {
-    CADD(CNT_DROP_OVERFLOW, 1u);
-    fail(D, x, MR_FAIL_SIM_CAPACITY);
-    return -1;
-  }
-  if (seq >= (1u << 24)) { fail(D, x, MR_FAIL_SIM_CAPACITY); return -1; }
-  uint32_t t = x.now + draw;
-  if (t >= T_KEY_MAX) { fail(D, x, MR_FAIL_SIM_CAPACITY); return -1; }
-  uint32_t slot = 0;
-  if constexpr (MW == 1) {
-    slot = (uint32_t)__builtin_ctzll(x.free_mask[0]);
-    x.free_mask[0] &= ~(1ull << slot);
-  } else {
-    bool got = false;
-#pragma unroll
-    for (uint32_t w = 0; w < MW; w++) {
-      if (!got && x.free_mask[w]) {
-        slot = 64u * w + (uint32_t)__builtin_ctzll(x.free_mask[w]);
-        x.free_mask[w] &= x.free_mask[w] - 1ull;
-        got = true;
-      }
-    }
-  }
-  uint4* mp = reinterpret_cast<uint4*>(MSP(slot));
-  mp[0] = make_uint4(hdr_make(type, src, dst, inc, k), term, a, b);
-  mp[1] = make_uint4(c, seq, (uint32_t)v, (uint32_t)(v >> 32));
-  x.inflight++;
-  CMAX(CNT_MAX_INFLIGHT, x.inflight);
-  if constexpr (MR_KEY32) {
-    LK(slot) = (t << 5) | dst;
-    if (t < (uint32_t)(x.mmin >> 32)) { x.mmin = ((uint64_t)t << 32) | dst; x.mslot = slot; }
-  } else {
-    const uint64_t key = ((uint64_t)t << 32) | (seq << 6) |
-                         (type == M_AE_REQ && (MR_AE_K0 || k) ? 32u : 0u) | dst;
-    LK(slot) = key;
-    if (key < x.mmin) { x.mmin = key; x.mslot = slot; }
-  }
-  return (int)slot;
-}
-
-// Phase A of a node event: decode, load the node, run the handler (state changes only; it
-// names the messages to send). Returns false when the event ends here (a dropped or stale
-// delivery, a clerk's reply, a KV request, a failure); its trace record is then taken.
 template <uint32_t S>
-DI bool node_event_a(const Dev& D, X& x, bool is_msg, uint32_t tnode, uint32_t slot,
-                     uint32_t seq, NR& nr, NE& e) {
+DI void node_event(const Dev& D, X& x, bool is_msg, uint32_t tnode, uint32_t slot,
+                   uint32_t seq, NR& nr) {
   constexpr bool KV = is_svc(S);  // kvraft / shard_ctrler request path
   uint32_t me = tnode, src = 0, type = 0, inc = 0, k = 0, mterm = 0, ma = 0, mb = 0, mc = 0;
-  e.kvready = false;
-  e.is_msg = is_msg;
+  bool kvready = false;
   uint32_t hdr_bits = 0;
 #ifndef MR_NODE_FIRST  // the node record's loads issued before the message is decoded
 #define MR_NODE_FIRST 1
@@ -1280,7 +1115,7 @@ DI bool node_event_a(const Dev& D, X& x, bool is_msg, uint32_t tnode, uint32_t s
       if (me >= CLERK_HOST) {  // KV_REP at a clerk host
         const uint64_t mv = ((uint64_t)MS32(MF_V + 1, slot) << 32) | MS32(MF_V, slot);
         clerk_deliver(D, x, me, src, inc, mterm, ma, mb, mc, mv, seq);
-        return false;
+        return;
       }
     }
   }
@@ -1316,22 +1151,22 @@ DI bool node_event_a(const Dev& D, X& x, bool is_msg, uint32_t tnode, uint32_t s
       CADD(CNT_DROP_DELIVER, 1u);
       nr_set(D, x, nr, 0, 16, me, seq, d);
       PROF(P_DROP);
-      return false;
+      return;
     }
     bool is_reply = (type == M_RV_REP || type == M_AE_REP || type == M_IS_REP);
     if (is_reply && inc != f_inc(d.f)) {
       CADD(CNT_DROP_STALE, 1u);
       nr_set(D, x, nr, 0, 17, me, seq, d);
       PROF(P_DROP);
-      return false;
+      return;
     }
     if constexpr (KV) {
       if (type == M_KV_REQ) {  // no Raft term: handled before the step-down rule
         kv_request(D, x, me, d, src, inc, mterm, ma, mb, mc);
-        if (x.code != RUN) return false;
+        if (x.code != RUN) return;
         store_node(D, x, me, d);
         nr_set(D, x, nr, 0, type, me, seq, d);
-        return false;
+        return;
       }
     }
     if (mterm > d.term) {  // step down
@@ -1364,7 +1199,7 @@ DI bool node_event_a(const Dev& D, X& x, bool is_msg, uint32_t tnode, uint32_t s
           if ((uint32_t)__builtin_popcount(votes) > D.n / 2) {  // become leader
             if (D.safety) {
               safety_on_leader(D, x, me, d);
-              if (x.code != RUN) return false;
+              if (x.code != RUN) return;
             }
             d.f = f_set(d.f, 0, 2, R_L);
             CADD(CNT_LEADERS, 1u);
@@ -1437,7 +1272,7 @@ DI bool node_event_a(const Dev& D, X& x, bool is_msg, uint32_t tnode, uint32_t s
               skipping = skipping && sk;
               bad |= skipping && ov[q] != pe[q].val;
             }
-            if (bad) { fail(D, x, MR_FAIL_SAFETY_LOG_MATCHING); return false; }
+            if (bad) { fail(D, x, MR_FAIL_SAFETY_LOG_MATCHING); return; }
           }
 #pragma unroll
           for (uint32_t q = 0; q < AC; q++) {
@@ -1448,7 +1283,7 @@ DI bool node_event_a(const Dev& D, X& x, bool is_msg, uint32_t tnode, uint32_t s
               rsprev = i == d.last ? lrs : ors[q];
               continue;
             }
-            if (i - d.snap > D.log_cap) { fail(D, x, MR_FAIL_SIM_CAPACITY); return false; }
+            if (i - d.snap > D.log_cap) { fail(D, x, MR_FAIL_SIM_CAPACITY); return; }
             guard_log_write(D, x, me, d.pexp, i);
             rsprev = pe[q].term == tprev ? rsprev : i;
             tprev = pe[q].term;
@@ -1496,10 +1331,10 @@ DI bool node_event_a(const Dev& D, X& x, bool is_msg, uint32_t tnode, uint32_t s
           d.snap = idx; d.snapt = mb; NSV(me) = MSV(slot);
           d.commit = idx; d.applied = idx;
           storage_snapshot(D, x, me, d.slen, idx);
-          if (x.code != RUN) return false;
+          if (x.code != RUN) return;
           if constexpr (kv_gen(S).maxraft > 0) {
-            kv_install(D, x, me, idx, e.kvready);
-            if (x.code != RUN) return false;
+            kv_install(D, x, me, idx, kvready);
+            if (x.code != RUN) return;
           }
           CADD(CNT_INSTALLS, 1u);
         }
@@ -1528,12 +1363,11 @@ DI bool node_event_a(const Dev& D, X& x, bool is_msg, uint32_t tnode, uint32_t s
     mode = SEND_VOTE; peers = others;
     PROF(P_ELECT);
   }
-#undef RESET_ME
-  if (!COOP_DRAW && nrst) {  // the last of this event's nrst draws (ectr advances by nrst, as drawn inline)
+  if (nrst) {  // the last of this event's nrst draws (ectr advances by nrst, as drawn inline)
     d.ectr += nrst - 1u;
     reset_timer(D, x, me, d);
-    nrst = 0;
   }
+#undef RESET_ME
   // peers a send can reach: one from a disconnected sender or to a disconnected destination
   // clogs (net_send, SEMANTICS §4), so it needs only its accounting — a sequence number, a
   // send index, drop_clog — and none of the send path's loads (MR_TAPE builds record its
@@ -1542,52 +1376,41 @@ DI bool node_event_a(const Dev& D, X& x, bool is_msg, uint32_t tnode, uint32_t s
 #define MR_CLOG_FAST 1
 #endif
   const uint32_t reach = (MR_TAPE || !MR_CLOG_FAST) ? ~0u : (bit(x.conn, me) ? x.conn : 0u);
-  if (mode == SEND_REPLY) peers = 1u << src;
 #if MR_SEND_EARLY
   // a leader's appends read our terms at next[p] - 1: issue those loads before the applier's
   // checker stores (the ring slot is valid whatever the applier does; gated after it)
+  uint32_t rawt[NB];
 #pragma unroll
   for (uint32_t p = 0; p < NB; p++) {
     const uint32_t ix = pv.nx[p] - 1u;
-    e.rawt[p] = (mode == SEND_APPEND && bit(peers & reach, p) && p < D.n && ix != 0u) ? D.log[logi(D, x, me, ix)].term : 0u;
+    rawt[p] = (mode == SEND_APPEND && bit(peers & reach, p) && p < D.n && ix != 0u) ? D.log[logi(D, x, me, ix)].term : 0u;
   }
 #endif
-  e.d = d;
-  e.pv = pv;
-  e.prange = prange;
-  e.me = me; e.src = src; e.inc = inc; e.seq = seq; e.kind = kind; e.mode = mode; e.peers = peers;
-  e.rtype = rtype; e.ra = ra; e.rb = rb; e.nrst = nrst; e.reach = reach;
-  return true;
-}
-
-// Phase C: the timer's cooperative draw, the sends (ascending peer order over the reachable
-// peers, after the applier), the KV replies, the node's store and trace record.
-template <uint32_t S>
-DI void node_event_c(const Dev& D, X& x, NE& e, NR& nr) {
-  constexpr bool KV = is_svc(S);
-  NC& d = e.d;
-  const uint32_t me = e.me;
-  if (COOP_DRAW && e.nrst) {  // the last of this event's nrst resets reaches the timer
-    d.ectr += e.nrst;
-    set_timer(x, me, x.now + LRES(0));
+  if (MR_AP_COOP && !KV && kv_gen(S).maxraft == 0) {
+    if (__ballot(d.applied < d.commit)) {  // committed entries reach the tester's applier
+      node_apply_coop<S>(D, x, me, d);
+      if (x.code != RUN) return;
+      PROF(P_APPLY);
+    }
+  } else if (d.applied < d.commit) {
+    node_apply<S>(D, x, me, d, kvready);
+    if (x.code != RUN) return;
+    PROF(P_APPLY);
   }
-  uint32_t peers = e.peers;
-  const uint32_t mode = e.mode;
+  if (mode == SEND_REPLY) peers = 1u << src;
   const uint32_t lt = mode == SEND_VOTE ? d.lastt : 0u;  // term_at(last)
   // appends: next[p] of every peer, then the terms at next[p] - 1, as two
   // batches of independent loads, staged in LDS for the send loop
   uint64_t snapv = 0;
   const uint32_t all = peers, seq0 = x.msgs_sent, ctr0 = d.nctr;
-  peers &= e.reach;
-  const uint32_t ht = COOP_DRAW && e.nrst ? 1u : 0u;  // index of the first send's draw
-  const uint32_t sendable = peers;
+  peers &= reach;
   if (mode == SEND_APPEND) {  // only a leader appends
     uint32_t nxa[NB];
     bool any_is = false;
-    const uint32_t lbase = sel_nb(e.pv.mt, me);
+    const uint32_t lbase = sel_nb(pv.mt, me);
 #pragma unroll
     for (uint32_t p = 0; p < NB; p++) {
-      nxa[p] = bit(peers, p) ? e.pv.nx[p] : 0u;
+      nxa[p] = bit(peers, p) ? pv.nx[p] : 0u;
       any_is |= bit(peers, p) && nxa[p] <= d.snap;
     }
 #pragma unroll
@@ -1596,7 +1419,7 @@ DI void node_event_c(const Dev& D, X& x, NE& e, NR& nr) {
       const bool ld = bit(peers, p) && nxa[p] > d.snap && pv != 0u && pv != d.snap &&
                       pv != d.last && pv <= lbase;
 #if MR_SEND_EARLY
-      const uint32_t t = ld ? e.rawt[p] : 0u;
+      const uint32_t t = ld ? rawt[p] : 0u;
 #else
       const uint32_t t = ld ? D.log[logi(D, x, me, pv)].term : 0u;
 #endif
@@ -1615,7 +1438,7 @@ DI void node_event_c(const Dev& D, X& x, NE& e, NR& nr) {
     uint32_t st = M_RV_REQ, sa = me, sb = d.last, sc = lt, sk = 0, sinc = f_inc(d.f), prev = 0;
     uint64_t sv = 0;
     if (mode == SEND_REPLY) {
-      st = e.rtype; sa = e.ra; sb = e.rb; sc = 0; sinc = e.inc;
+      st = rtype; sa = ra; sb = rb; sc = 0; sinc = inc;
     } else if (mode == SEND_APPEND) {
       const uint32_t nx = LNX(p);
       if (nx <= d.snap) {
@@ -1628,15 +1451,9 @@ DI void node_event_c(const Dev& D, X& x, NE& e, NR& nr) {
       }
     }
     PROF(P_S_SETUP);
-    int s;
-    if constexpr (COOP_DRAW) {
-      const uint32_t draw = LRES(ht + (uint32_t)__builtin_popcount(sendable & ((1u << p) - 1u)));
-      s = net_send_drawn(D, x, me, d.nctr, p, st, sinc, d.term, sa, sb, sc, sv, sk, draw);
-    } else {
-      s = net_send(D, x, me, d.nctr, p, st, sinc, d.term, sa, sb, sc, sv, sk);
-    }
+    int s = net_send(D, x, me, d.nctr, p, st, sinc, d.term, sa, sb, sc, sv, sk);
     if (x.code != RUN) {  // the clogged sends before this one are counted as they happened
-      CADD(CNT_DROP_CLOG, (uint32_t)__builtin_popcount(below & ~e.reach));
+      CADD(CNT_DROP_CLOG, (uint32_t)__builtin_popcount(below & ~reach));
       return;
     }
     PROF(P_S_NET);
@@ -1648,54 +1465,18 @@ DI void node_event_c(const Dev& D, X& x, NE& e, NR& nr) {
   }
   x.msgs_sent = seq0 + (uint32_t)__builtin_popcount(all);  // every send of the event, clogged too
   d.nctr = ctr0 + (uint32_t)__builtin_popcount(all);
-  CADD(CNT_DROP_CLOG, (uint32_t)__builtin_popcount(all & ~e.reach));
-  if (plo_acc <= phi_acc) pend_note(D, x, me, d, plo_acc, phi_acc, e.prange.x, e.prange.y);
+  CADD(CNT_DROP_CLOG, (uint32_t)__builtin_popcount(all & ~reach));
+  if (plo_acc <= phi_acc) pend_note(D, x, me, d, plo_acc, phi_acc, prange.x, prange.y);
   if constexpr (KV) {
-    if (e.kvready) {
+    if (kvready) {
       kv_flush(D, x, me, d);
       if (x.code != RUN) return;
     }
   }
   PROF(P_SEND);
   store_node(D, x, me, d);
-  nr_set(D, x, nr, e.is_msg ? 0u : 1u, e.kind, me, e.is_msg ? e.seq : 0u, d);
+  nr_set(D, x, nr, is_msg ? 0u : 1u, kind, me, is_msg ? seq : 0u, d);
   PROF(P_STORE);
-}
-
-// The draws phase C will read (coop_draws owner side): the timer's and the reachable sends'.
-DI void node_draw_items(const X& x, const NE& e, uint32_t& cnt, uint32_t& wme, uint32_t& ctr0,
-                        uint32_t& ectr) {
-  const uint32_t ht = e.nrst ? 1u : 0u;
-  const uint32_t sendable = e.peers & e.reach;
-  cnt = ht + (uint32_t)__builtin_popcount(sendable);
-  wme = e.me | ((x.netmode & 1u) << 5) | (ht << 6) | ((sendable & 255u) << 8) | ((e.peers & 255u) << 16);
-  ctr0 = e.d.nctr;
-  ectr = e.d.ectr + e.nrst - 1u;
-}
-
-// The wave-uniform section of a node iteration: every lane of the wave is here (go = it has a
-// node event in phase C). The tester's applier (cooperative for the Raft-only scenarios,
-// sequential per lane for the KV services) and the events' draws (coop_draws).
-template <uint32_t S>
-DI void node_mid(const Dev& D, X& x, bool& go, NE& e) {
-  constexpr bool KV = is_svc(S);
-  if (MR_AP_COOP && !KV && kv_gen(S).maxraft == 0) {
-    if (__ballot(go && e.d.applied < e.d.commit)) {  // committed entries reach the tester's applier
-      node_apply_coop<S>(D, x, e.me, e.d, go);
-      if (x.code != RUN) go = false;
-      PROF(P_APPLY);
-    }
-  } else if (go && e.d.applied < e.d.commit) {
-    node_apply<S>(D, x, e.me, e.d, e.kvready);
-    if (x.code != RUN) go = false;
-    PROF(P_APPLY);
-  }
-  if constexpr (COOP_DRAW) {
-    uint32_t cnt = 0, wme = 0, ctr0 = 0, ectr = 0;
-    if (go) node_draw_items(x, e, cnt, wme, ctr0, ectr);
-    coop_draws(D, x, cnt, wme, ctr0, ectr);
-    PROF(P_DRAW);
-  }
 }
 
 // ---------------------------------------------------------------- tester API (tester.rs)
@@ -1877,6 +1658,18 @@ DI void tester(const Dev& D, X& x) {
 #pragma unroll
   for (uint32_t k = 0; k < T_NH; k++) t.h[k] = CS(CS_TH + k);
   t.hv = C64(C64_THV);
+#ifndef MR_T_PREFETCH  // A/B: the leader's record fetched with the frame (figure_8 start() loop)
+#define MR_T_PREFETCH 0
+#endif
+  if constexpr (MR_T_PREFETCH && (S == MR_SCN_FIGURE_8_UNRELIABLE_2C || S == MR_SCN_FIGURE_8_2C ||
+                                  S == MR_SCN_FIGURE_8_UNRELIABLE_CRASH)) {
+    // the record of the lowest leader: its first 64 B (scalars, pending payload range) reach
+    // the cache with the frame's loads, so start() on it waits for a cache hit, not HBM
+    if (x.lmask) {
+      const uint32_t pf = ND(NF_FLAGS, (uint32_t)__builtin_ctz(x.lmask));
+      asm volatile("" ::"v"(pf));
+    }
+  }
   x.yield = 0;
   for (int guard = 0;; guard++) {
     if (guard > 4096) { fail(D, x, MR_FAIL_SIM_BAD_PROGRAM); return; }
@@ -2001,7 +1794,9 @@ template <uint32_t S, uint32_t NBT>
 __global__ void __launch_bounds__(STEP_BLOCK, step_waves<S>()) step_kernel(Dev D, uint32_t budget) {
   static_assert(NBT == NB, "one node bound per translation unit");
   X x;
-  x.c = blockIdx.x * blockDim.x + threadIdx.x;
+  // lanes 0 .. lpw - 1 of each 64-lane block hold clusters (D.lpw < 64: a batch smaller than the
+  // resident lanes still spreads over two waves per SIMD; the other lanes idle)
+  x.c = blockIdx.x * D.lpw + threadIdx.x;
 #ifdef MR_PROF
   if ((threadIdx.x & 63) == 0) {
     for (uint32_t k = 0; k < 2 * P__N; k++) s_prof[threadIdx.x >> 6][k] = 0;
@@ -2009,7 +1804,7 @@ __global__ void __launch_bounds__(STEP_BLOCK, step_waves<S>()) step_kernel(Dev D
   }
 #endif
   x.c += D.c0;  // lane l starts with cluster c0 + l of this launch's chunk
-  const bool in = x.c < D.c0 + D.L && x.c < D.C;
+  const bool in = threadIdx.x < D.lpw && x.c < D.c0 + D.L && x.c < D.C;
   x.code = MR_PASS;
   if (in) lane_load<S>(D, x);
   bool held = x.code == RUN;  // this lane runs cluster x.c (its state is in registers / LDS)
@@ -2068,7 +1863,10 @@ __global__ void __launch_bounds__(STEP_BLOCK, step_waves<S>()) step_kernel(Dev D
     // AppendEntries deliveries (the longest node path: probe, payload batches, log writes) wait
     // until they are >= AE_NUM / AE_DEN of the wave's node events, so the other node events run
     // without their round trips; like any lane that waits, a cluster's own order is unchanged
-    if constexpr (MR_AE_CLASS && !MR_KEY32 && S == MR_SCN_FIGURE_8_UNRELIABLE_2C) {
+#ifndef MR_AE_ALL  // A/B: the AppendEntries sub-class for every 64-bit-key scenario
+#define MR_AE_ALL 0
+#endif
+    if constexpr (MR_AE_CLASS && !MR_KEY32 && (MR_AE_ALL || S == MR_SCN_FIGURE_8_UNRELIABLE_2C)) {
       if (!tpick) {
         const bool ae = run && cls == CLS_MSG && ((key >> 5) & 1u);
         const uint32_t nae = __popcll(__ballot(ae));
@@ -2081,51 +1879,32 @@ __global__ void __launch_bounds__(STEP_BLOCK, step_waves<S>()) step_kernel(Dev D
       }
     }
     PROF(P_SEL);
-    bool act = run && mine;
-    if (act && nthr(S) > 0 && (uint32_t)(key >> 32) == INF_T) {  // nothing can wake the test body
+    if (!run || !mine) continue;
+    if (nthr(S) > 0 && (uint32_t)(key >> 32) == INF_T) {  // nothing can wake the test body
       fail(D, x, MR_FAIL_SIM_BAD_PROGRAM);
-      act = false;
-    }
-    if (act) {
-      x.now = (uint32_t)(key >> 32);
-      need = true;
-      x.events++;
-      if (x.events > D.max_events) { fail(D, x, MR_FAIL_SIM_EVENT_LIMIT); act = false; }
-    }
-#ifdef MR_ALL_CLASSES
-    const bool tlane = act && cls == CLS_TESTER;
-#else
-    const bool tlane = tpick;  // wave-uniform: the lanes of a tester iteration run tester events only
-#endif
-    if (tlane) {
-      if (act) {
-        CADD(CNT_EV_TESTER, 1u);
-        if constexpr (nthr(S) > 0) {
-          if (tcli) thr_step<S>(D, x, x.cslot);
-          else tester<S>(D, x);
-        } else {
-          tester<S>(D, x);
-        }
-        PROF(P_TESTER);
-      }
       continue;
     }
-    // a node iteration: phase A per lane, then a wave-uniform section every lane of the wave
-    // helps with (the tester's applier, the events' draws), then phase C per lane
-    NR nr;
-    nr.on = false;
-    NE e;
-    e.nrst = 0; e.peers = 0; e.reach = 0; e.d.commit = 0; e.d.applied = 0;
-    bool go = false;
-    if (act) {
+    x.now = (uint32_t)(key >> 32);
+    need = true;
+    x.events++;
+    if (x.events > D.max_events) { fail(D, x, MR_FAIL_SIM_EVENT_LIMIT); continue; }
+    if (cls != CLS_TESTER) {
       CADD(cls == CLS_MSG ? CNT_EV_MSG : CNT_EV_TIMER, 1u);
-      go = node_event_a<S>(D, x, cls == CLS_MSG, node, x.mslot, ((uint32_t)key & 0x3FFFFFFFu) >> 6,
-                           nr, e);
+      NR nr;
+      nr.on = false;
+      node_event<S>(D, x, cls == CLS_MSG, node, x.mslot, ((uint32_t)key & 0x3FFFFFFFu) >> 6, nr);
+      if (MR_REC_ONCE && nr.on && x.code == RUN)
+        rec8(D, x, x.now, nr.w1, nr.aux, nr.term, nr.commit, nr.applied, nr.last, nr.snap);
+    } else {
+      CADD(CNT_EV_TESTER, 1u);
+      if constexpr (nthr(S) > 0) {
+        if (tcli) thr_step<S>(D, x, x.cslot);
+        else tester<S>(D, x);
+      } else {
+        tester<S>(D, x);
+      }
+      PROF(P_TESTER);
     }
-    node_mid<S>(D, x, go, e);
-    if (go) node_event_c<S>(D, x, e, nr);
-    if (MR_REC_ONCE && nr.on && x.code == RUN)
-      rec8(D, x, x.now, nr.w1, nr.aux, nr.term, nr.commit, nr.applied, nr.last, nr.snap);
   }
 #ifdef MR_PROF
   PROF(P_TAIL);
@@ -2241,7 +2020,7 @@ hipError_t launch_reduce(const Dev& D, unsigned long long* out, uint64_t cluster
 
 template <uint32_t S, uint32_t NBT>
 hipError_t launch_step_t(const Dev& D, uint32_t budget, hipStream_t s) {
-  dim3 blk(STEP_BLOCK), grd((D.L + STEP_BLOCK - 1) / STEP_BLOCK);
+  dim3 blk(STEP_BLOCK), grd((D.L + D.lpw - 1) / D.lpw);
   const size_t lds = (size_t)D.M * STEP_BLOCK * sizeof(lkey_t) +  // message keys
                     2 * MR_MAX_NODES * STEP_BLOCK * sizeof(uint32_t);  // send-loop staging
   hipLaunchKernelGGL((step_kernel<S, NBT>), grd, blk, lds, s, D, budget);

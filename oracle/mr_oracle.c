@@ -46,6 +46,7 @@ enum { KV_OK = 0, KV_WRONG_LEADER = 1, KV_FAILED = 2 };
 #define MAX_CLERKS 128u /* clerk ids (make_client order) */
 #define KV_KEYS 64u     /* keys a KV server may hold */
 #define KV_APP 5u       /* distinct appenders tracked per key */
+#define LIN_CLI 15u     /* generic_test_linearizability: clients, keys, appender states per key (§9b) */
 #define KV_ALL 0xFFFFFFu /* Get elem: the states of appenders 0..4, packed */
 #define KV_HP 0x100000001B3ull /* value hash multiplier (SEMANTICS §9) */
 #define KV_SLOTS 6u     /* thread / clerk slots: 0 = main + ck, 1 + cli = client cli */
@@ -106,6 +107,7 @@ typedef struct {
   uint32_t owner, mcl; /* the thread its calls wake (0 = the test body); mcl: a test-body clerk */
   uint32_t op, key, elem;
   uint32_t llo; /* a Get's lower bound at its call (SEMANTICS §9a) */
+  uint32_t lepoch, lnopend; /* §9b: the key's Put epoch at the call; no Put pending at the call */
 } OClerk;
 typedef struct {
   uint32_t tid, live, pc, j, cli, tctr, gen;
@@ -119,7 +121,8 @@ typedef struct {
 typedef struct { uint32_t used, idx, clerk, seq, tag, ready, status, value, host; uint64_t vh; } OPend;
 /* a key's value (SEMANTICS §9): the hash of its token sequence, its byte length, and
  * per appender (cli + 1 | count << 8 | bad << 31) for the append-order checks */
-typedef struct { uint64_t h; uint32_t len; uint32_t app[KV_APP]; } OKey;
+/* (generic_test_linearizability, SEMANTICS §9b: app[cli] = count | last j << 12 | bad << 31) */
+typedef struct { uint64_t h; uint32_t len; uint32_t app[LIN_CLI]; } OKey;
 /* a KV server's state machine as its snapshot holds it (SEMANTICS §9) */
 typedef struct { uint32_t dedup[MAX_CLERKS]; OKey keys[KV_KEYS]; } OKvState;
 #define KV_SNAP_EVERY 16u /* the service snapshots at applied indices that are multiples of 16 */
@@ -155,6 +158,9 @@ typedef struct {
   uint32_t led[64];   /* MR_F_SAFETY: bit t = a leader was elected in term t (t < 2048) */
   uint32_t lin[KV_KEYS][KV_APP][5]; /* linearizability: per (key, appender) tag, called, acked,
                                      * seen, and a pending all-appenders Get's lower bound */
+  uint32_t lin15; /* generic_test_linearizability (SEMANTICS §9b): keys of 15 client states */
+  uint32_t l15_called[16][LIN_CLI], l15_acked[16][LIN_CLI], l15_epoch[16], l15_pend[16];
+  uint32_t l15_j[LIN_CLI]; /* client cli's next token j, carried over iterations (tokens unique) */
   uint8_t link[MR_MAX_NODES]; /* server links (connect2/disconnect2): bit j of link[i] = i~j */
   uint64_t tape_row; int tape_on; uint64_t tape_pos; /* keyed decisions: row, count (§12) */
   uint8_t ccut[CK_SLOTS];     /* clerk links cut: bit j of ccut[k] = clerk host 8 + k !~ server j */
@@ -460,7 +466,8 @@ static uint32_t ndig(uint32_t v) { uint32_t d = 1; while (v >= 10) { v /= 10; d+
 static uint32_t put_len(uint32_t t) { return t == 0 ? 0 : t < (1u << 20) ? ndig(t - 1) : 1; }
 
 /* the state of appender `cli` of a key: count | ok << 31 (ok: its tokens arrived in order, once) */
-static uint32_t kv_app_state(const OKey* k, uint32_t cli) {
+static uint32_t kv_app_state(const OKey* k, uint32_t cli, int lin15) {
+  if (lin15) return cli < LIN_CLI ? (k->app[cli] & 0xFFFu) | ((~k->app[cli] >> 31) << 31) : 1u << 31;
   for (uint32_t a = 0; a < KV_APP; a++)
     if ((k->app[a] & 0xFFu) == cli + 1) return ((k->app[a] >> 8) & 0x7FFFFFu) | ((~k->app[a] >> 31) << 31);
   return 1u << 31;
@@ -468,11 +475,11 @@ static uint32_t kv_app_state(const OKey* k, uint32_t cli) {
 
 /* a Get's reply value: the state of appender elem, or (KV_ALL) of appenders 0..4 packed as
  * count (5 bits, saturating at 31) | ok << 5 each */
-static uint32_t kv_get_value(const OKey* k, uint32_t elem) {
-  if (elem != KV_ALL) return kv_app_state(k, elem);
+static uint32_t kv_get_value(const OKey* k, uint32_t elem, int lin15) {
+  if (elem != KV_ALL || lin15) return kv_app_state(k, elem, lin15);
   uint32_t out = 0;
   for (uint32_t c = 0; c < KV_APP; c++) {
-    uint32_t st = kv_app_state(k, c), n = st & 0xFFFFFFu;
+    uint32_t st = kv_app_state(k, c, 0), n = st & 0xFFFFFFu;
     out |= ((n > 31 ? 31 : n) | ((st >> 31) ? 32u : 0u)) << (6 * c);
   }
   return out;
@@ -492,9 +499,29 @@ static void kv_apply(OSim* s, uint32_t me, uint32_t i, uint64_t v) {
     query = s->ops[elem].type == CT_QUERY;
   } else if (op == KV_GET) {
     outh = k->h;
-    out = kv_get_value(k, elem);
+    out = kv_get_value(k, elem, s->lin15);
   } else if (seq > s->kv_dedup[me][clerk] || (s->cfg.flags & MR_F_BUG_NO_DEDUP)) {
-    if (op == KV_PUT) { /* elem = the value's token (0 = "") */
+    if (s->lin15) { /* SEMANTICS §9b: a Put / Append of token "x {cli} {j} y", elem = cli << 19 | j */
+      uint32_t cli = elem >> 19, j = elem & 0x7FFFFu;
+      if (cli >= LIN_CLI) t_fail(s, MR_FAIL_SIM_CAPACITY);
+      if (op == KV_PUT) {
+        memset(k, 0, sizeof *k);
+        k->h = elem + 1ull; /* the hash of "" then the token */
+        k->len = 5 + ndig(cli) + ndig(j);
+        k->app[cli] = 1u | (j << 12);
+      } else {
+        uint32_t w = k->app[cli], n = w & 0xFFFu;
+        if (!(w >> 31) && (n == 0 || j > ((w >> 12) & 0x7FFFFu))) {
+          if (n + 1 > 0xFFFu) t_fail(s, MR_FAIL_SIM_CAPACITY);
+          w = (n + 1) | (j << 12);
+        } else {
+          w |= 1u << 31;
+        }
+        k->app[cli] = w;
+        k->h = k->h * KV_HP + elem + 1;
+        k->len += 5 + ndig(cli) + ndig(j);
+      }
+    } else if (op == KV_PUT) { /* elem = the value's token (0 = "") */
       memset(k, 0, sizeof *k);
       if (elem) { k->h = (elem + 1ull) * 0x9E3779B97F4A7C15ull; k->len = put_len(elem); }
     } else { /* Append of token "x {cli} {j} y": elem = cli << 19 | j */
@@ -734,7 +761,7 @@ static void kv_request(OSim* s, uint32_t me, OMsg* m) {
     /* the buggy leader answers from its own state at once: no log entry, no quorum */
     OKey* k = &s->kv[me][(m->a >> 2) & 63u];
     uint32_t elem = m->c & 0xFFFFFFu;
-    kv_send_rep(s, me, m->src, clerk, m->term, KV_OK, me, kv_get_value(k, elem), k->h);
+    kv_send_rep(s, me, m->src, clerk, m->term, KV_OK, me, kv_get_value(k, elem, s->lin15), k->h);
     return;
   }
   uint32_t p = 0;
@@ -1518,8 +1545,38 @@ static uint32_t* lin_ent(OSim* s, uint32_t key, uint32_t cli) {
   t_fail(s, MR_FAIL_SIM_CAPACITY);
   return NULL;
 }
+/* SEMANTICS §9b: the Put-epoch checker of generic_test_linearizability (keys 0..14) */
+static void lin15_call(OSim* s, OClerk* c) {
+  uint32_t k = c->key & 15u;
+  if (c->op == KV_PUT) {
+    s->l15_epoch[k]++;
+    s->l15_pend[k]++;
+    s->l15_called[k][(c->elem >> 19) % LIN_CLI]++;
+    memset(s->l15_acked[k], 0, sizeof s->l15_acked[k]);
+  } else if (c->op == KV_APPEND) {
+    s->l15_called[k][(c->elem >> 19) % LIN_CLI]++;
+    c->lepoch = s->l15_epoch[k];
+    c->lnopend = s->l15_pend[k] == 0;
+  } else {
+    c->llo = s->l15_acked[k][c->elem % LIN_CLI];
+    c->lepoch = s->l15_epoch[k];
+  }
+}
+static void lin15_return(OSim* s, OClerk* c) {
+  uint32_t k = c->key & 15u;
+  if (c->op == KV_PUT) { s->l15_pend[k]--; return; }
+  if (c->op == KV_APPEND) {
+    if (c->lnopend && s->l15_epoch[k] == c->lepoch) s->l15_acked[k][(c->elem >> 19) % LIN_CLI]++;
+    return;
+  }
+  uint32_t lo = s->l15_epoch[k] == c->lepoch ? c->llo : 0, n = c->rval & 0xFFFFFFu;
+  s->r.kv_lin_checked++;
+  if (!(c->rval >> 31) || n < lo || n > s->l15_called[k][c->elem % LIN_CLI])
+    t_fail(s, MR_FAIL_KV_NOT_LINEARIZABLE);
+}
 static void lin_call(OSim* s, OClerk* c) {
   if (s->ctrl_mode) return;
+  if (s->lin15) { lin15_call(s, c); return; }
   if (c->op == KV_PUT) { /* a new value */
     memset(s->lin[c->key & (KV_KEYS - 1)], 0, sizeof s->lin[0]);
     return;
@@ -1537,6 +1594,7 @@ static void lin_call(OSim* s, OClerk* c) {
 }
 static void lin_return(OSim* s, OClerk* c) {
   if (s->ctrl_mode) return;
+  if (s->lin15) { lin15_return(s, c); return; }
   if (c->op == KV_APPEND) { lin_ent(s, c->key, c->elem >> 19)[2]++; return; }
   if (c->op != KV_GET) return;
   if (c->elem == KV_ALL) { /* count (5 bits, 31 = saturated) | ok << 5 per appender */
@@ -1622,6 +1680,40 @@ static void kv_client_step(OSim* s, uint32_t slot) {
         if (c->rvh != t->hlast) t_fail(s, MR_FAIL_KV_GET_WRONG); /* kvraft/tests.rs:127 */
         t->pc = 2;
         break;
+      default: t_fail(s, MR_FAIL_SIM_BAD_PROGRAM);
+    }
+  }
+block:
+  rec_simple(s, 2, t->tid & 0xFFu);
+  return;
+finish:
+  rec_simple(s, 2, t->tid & 0xFFu);
+  thr_finish(s, slot);
+}
+
+/* client task of generic_test_linearizability (SEMANTICS §9b): random keys and operations */
+static uint32_t thr_range(OSim* s, OThr* t, uint32_t lo, uint32_t hi);
+static void lin_client_step(OSim* s, uint32_t slot) {
+  OThr* t = &s->th[slot];
+  for (;;) {
+    switch (t->pc) {
+      case 0: {
+        if (s->kv_done) goto finish;
+        uint32_t key = thr_range(s, t, 0, LIN_CLI), e = (t->cli << 19) | t->j;
+        if (thr_range(s, t, 0, 1000) < 500) {
+          clerk_begin(s, slot, KV_APPEND, key, e);
+          t->pc = 1;
+        } else if (thr_range(s, t, 0, 1000) < 100) {
+          clerk_begin(s, slot, KV_PUT, key, e);
+          t->pc = 1;
+        } else {
+          clerk_begin(s, slot, KV_GET, key, thr_range(s, t, 0, LIN_CLI));
+          t->pc = 2;
+        }
+        goto block;
+      }
+      case 1: if (!clerk_resume(s, slot)) goto block; t->j++; t->pc = 0; break;
+      case 2: if (!clerk_resume(s, slot)) goto block; t->pc = 0; break;
       default: t_fail(s, MR_FAIL_SIM_BAD_PROGRAM);
     }
   }
@@ -1779,6 +1871,7 @@ static void client_step(OSim* s, uint32_t slot) {
     case MR_SCN_CTRL_MULTI_4A: ctl_client_step(s, slot); break;
     default:
       if (s->th[slot].kind == 1) part_step(s, slot);
+      else if (s->th[slot].kind == 4) lin_client_step(s, slot);
       else if (s->th[slot].kind >= 2) kv_task_step(s, slot);
       else kv_client_step(s, slot);
       break;
@@ -2082,9 +2175,12 @@ static void t_start_server(OSim* s, uint32_t i) {
   memset(s->kv_dedup[i], 0, sizeof s->kv_dedup[i]);
 }
 
+/* kvraft/tests.rs:65-220; with `lin`, generic_test_linearizability (SEMANTICS §9b, the
+ * reference's sketched kvraft/tests.rs:386-390, 524-528) */
 static void scn_kv_generic(OSim* s, uint32_t nclients, int unreliable, int crash, int partitions,
-                           uint32_t maxraftstate) { /* kvraft/tests.rs:65-220 */
+                           uint32_t maxraftstate, int lin) {
   s->kv_maxraft = maxraftstate;
+  s->lin15 = lin;
   t_new(s, 0); /* Tester::new (kvraft/tester.rs:27-56): start_server for every server */
   if (unreliable) t_set_unreliable(s, 1);
   s->kv_mode = 1;
@@ -2093,7 +2189,10 @@ static void scn_kv_generic(OSim* s, uint32_t nclients, int unreliable, int crash
   uint32_t ps = 1 + nclients; /* the partitioner's slot */
   for (uint32_t i = 0; i < 3; i++) {
     s->kv_done = 0;
-    for (uint32_t cli = 0; cli < nclients; cli++) kv_spawn(s, 1 + cli, 1 + nclients * i + cli, cli);
+    for (uint32_t cli = 0; cli < nclients; cli++) {
+      kv_spawn(s, 1 + cli, 1 + nclients * i + cli, cli);
+      if (lin) { s->th[1 + cli].kind = 4; s->th[1 + cli].j = s->l15_j[cli]; }
+    }
     if (partitions) {
       t_sleep(s, 1000000u);
       thr_spawn(s, ps, 1 + 3 * nclients + i);
@@ -2116,6 +2215,10 @@ static void scn_kv_generic(OSim* s, uint32_t nclients, int unreliable, int crash
     }
     for (uint32_t cli = 0; cli < nclients; cli++) {
       t_join(s, 1 + cli);
+      if (lin) { /* no predicted values: the checker judged every Get (SEMANTICS §9b) */
+        s->l15_j[cli] = s->th[1 + cli].j;
+        continue;
+      }
       uint32_t j = s->th[1 + cli].j;
       uint32_t v = main_call(s, KV_GET, cli, cli); /* check_clnt_appends(cli, &v, j) */
       s->r.kv_checked++;
@@ -2377,26 +2480,32 @@ static int run_scenario(OSim* s) {
     case MR_SCN_UNRELIABLE_CHURN_2C: scn_churn(s, 1); break;
     case MR_SCN_CTRL_BASIC_4A: scn_ctrl_basic(s); break;
     case MR_SCN_CTRL_MULTI_4A: scn_ctrl_multi(s); break;
-    case MR_SCN_KV_BASIC_3A: scn_kv_generic(s, 1, 0, 0, 0, 0); break;
-    case MR_SCN_KV_CONCURRENT_3A: scn_kv_generic(s, 5, 0, 0, 0, 0); break;
-    case MR_SCN_KV_UNRELIABLE_3A: scn_kv_generic(s, 5, 1, 0, 0, 0); break;
-    case MR_SCN_KV_MANY_PARTITIONS_ONE_CLIENT_3A: scn_kv_generic(s, 1, 0, 0, 1, 0); break;
-    case MR_SCN_KV_MANY_PARTITIONS_MANY_CLIENTS_3A: scn_kv_generic(s, 5, 0, 0, 1, 0); break;
-    case MR_SCN_KV_PERSIST_ONE_CLIENT_3A: scn_kv_generic(s, 1, 0, 1, 0, 0); break;
-    case MR_SCN_KV_PERSIST_CONCURRENT_3A: scn_kv_generic(s, 5, 0, 1, 0, 0); break;
-    case MR_SCN_KV_PERSIST_CONCURRENT_UNRELIABLE_3A: scn_kv_generic(s, 5, 1, 1, 0, 0); break;
-    case MR_SCN_KV_PERSIST_PARTITION_3A: scn_kv_generic(s, 5, 0, 1, 1, 0); break;
-    case MR_SCN_KV_PERSIST_PARTITION_UNRELIABLE_3A: scn_kv_generic(s, 5, 1, 1, 1, 0); break;
+    case MR_SCN_KV_BASIC_3A: scn_kv_generic(s, 1, 0, 0, 0, 0, 0); break;
+    case MR_SCN_KV_CONCURRENT_3A: scn_kv_generic(s, 5, 0, 0, 0, 0, 0); break;
+    case MR_SCN_KV_UNRELIABLE_3A: scn_kv_generic(s, 5, 1, 0, 0, 0, 0); break;
+    case MR_SCN_KV_MANY_PARTITIONS_ONE_CLIENT_3A: scn_kv_generic(s, 1, 0, 0, 1, 0, 0); break;
+    case MR_SCN_KV_MANY_PARTITIONS_MANY_CLIENTS_3A: scn_kv_generic(s, 5, 0, 0, 1, 0, 0); break;
+    case MR_SCN_KV_PERSIST_ONE_CLIENT_3A: scn_kv_generic(s, 1, 0, 1, 0, 0, 0); break;
+    case MR_SCN_KV_PERSIST_CONCURRENT_3A: scn_kv_generic(s, 5, 0, 1, 0, 0, 0); break;
+    case MR_SCN_KV_PERSIST_CONCURRENT_UNRELIABLE_3A: scn_kv_generic(s, 5, 1, 1, 0, 0, 0); break;
+    case MR_SCN_KV_PERSIST_PARTITION_3A: scn_kv_generic(s, 5, 0, 1, 1, 0, 0); break;
+    case MR_SCN_KV_PERSIST_PARTITION_UNRELIABLE_3A: scn_kv_generic(s, 5, 1, 1, 1, 0, 0); break;
     case MR_SCN_KV_UNRELIABLE_ONE_KEY_3A: scn_kv_one_key(s); break;
     case MR_SCN_KV_ONE_PARTITION_3A: scn_kv_one_partition(s); break;
     case MR_SCN_KV_SNAPSHOT_RPC_3B: scn_kv_snapshot_rpc(s); break;
     case MR_SCN_KV_SNAPSHOT_SIZE_3B: scn_kv_snapshot_size(s); break;
-    case MR_SCN_KV_SNAPSHOT_RECOVER_3B: scn_kv_generic(s, 1, 0, 1, 0, 1000); break;
-    case MR_SCN_KV_SNAPSHOT_RECOVER_MANY_CLIENTS_3B: scn_kv_generic(s, 20, 0, 1, 0, 1000); break;
-    case MR_SCN_KV_SNAPSHOT_UNRELIABLE_3B: scn_kv_generic(s, 5, 1, 0, 0, 1000); break;
-    case MR_SCN_KV_SNAPSHOT_UNRELIABLE_RECOVER_3B: scn_kv_generic(s, 5, 1, 1, 0, 1000); break;
+    case MR_SCN_KV_SNAPSHOT_RECOVER_3B: scn_kv_generic(s, 1, 0, 1, 0, 1000, 0); break;
+    case MR_SCN_KV_SNAPSHOT_RECOVER_MANY_CLIENTS_3B: scn_kv_generic(s, 20, 0, 1, 0, 1000, 0); break;
+    case MR_SCN_KV_SNAPSHOT_UNRELIABLE_3B: scn_kv_generic(s, 5, 1, 0, 0, 1000, 0); break;
+    case MR_SCN_KV_SNAPSHOT_UNRELIABLE_RECOVER_3B: scn_kv_generic(s, 5, 1, 1, 0, 1000, 0); break;
+    case MR_SCN_KV_PERSIST_PARTITION_UNRELIABLE_LINEARIZABLE_3A:
+      scn_kv_generic(s, LIN_CLI, 1, 1, 1, 0, 1);
+      break;
+    case MR_SCN_KV_SNAPSHOT_UNRELIABLE_RECOVER_CONCURRENT_PARTITION_LINEARIZABLE_3B:
+      scn_kv_generic(s, LIN_CLI, 1, 1, 1, 1000, 1);
+      break;
     case MR_SCN_KV_SNAPSHOT_UNRELIABLE_RECOVER_CONCURRENT_PARTITION_3B:
-      scn_kv_generic(s, 5, 1, 1, 1, 1000);
+      scn_kv_generic(s, 5, 1, 1, 1, 1000, 0);
       break;
     default: return -1;
   }
@@ -2412,7 +2521,7 @@ static int sim_alloc(OSim* s, const mr_cfg* cfg) {
   if (cfg->n_nodes < 3 || cfg->n_nodes > MR_MAX_NODES) return -1;
   if (cfg->log_cap < 16 || (cfg->log_cap & (cfg->log_cap - 1))) return -1;
   if (cfg->msg_slots < 1 || cfg->msg_slots > MR_MAX_MSG_SLOTS) return -1;
-  if (cfg->msg_slots > 64 && cfg->scenario != MR_SCN_KV_SNAPSHOT_RECOVER_MANY_CLIENTS_3B) return -1;
+  if (cfg->msg_slots > 64 && !mr_scn_wide_slots(cfg->scenario)) return -1;
   if (cfg->ae_max < 1 || cfg->ae_max > MR_MAX_AE) return -1;
   if (cfg->apply_cap < 16) return -1;
   for (uint32_t i = 0; i < cfg->n_nodes; i++) {
@@ -2462,6 +2571,10 @@ static void sim_reset(OSim* s, uint64_t cluster) {
   s->ctrl_mode = 0; s->nops = 0;
   memset(s->led, 0, sizeof s->led);
   memset(s->lin, 0, sizeof s->lin);
+  s->lin15 = 0;
+  memset(s->l15_called, 0, sizeof s->l15_called); memset(s->l15_acked, 0, sizeof s->l15_acked);
+  memset(s->l15_epoch, 0, sizeof s->l15_epoch); memset(s->l15_pend, 0, sizeof s->l15_pend);
+  memset(s->l15_j, 0, sizeof s->l15_j);
   s->kv_maxraft = 0;
   memset(s->kvs, 0, MR_MAX_NODES * sizeof(OKvState));
   memset(s->kring_idx, 0, KV_RING * sizeof(uint32_t));
@@ -2586,7 +2699,9 @@ static const char* k_names[MR_SCN_COUNT_] = {
     "persist_partition_unreliable_3a", "unreliable_one_key_3a", "one_partition_3a",
     "snapshot_rpc_3b", "snapshot_size_3b", "snapshot_recover_3b", "snapshot_recover_many_clients_3b",
     "snapshot_unreliable_3b", "snapshot_unreliable_recover_3b",
-    "snapshot_unreliable_recover_concurrent_partition_3b"};
+    "snapshot_unreliable_recover_concurrent_partition_3b",
+    "persist_partition_unreliable_linearizable_3a",
+    "snapshot_unreliable_recover_concurrent_partition_linearizable_3b"};
 
 uint32_t mro_scenario_from_name(const char* name) {
   for (uint32_t i = 1; i < MR_SCN_COUNT_; i++)
@@ -2597,7 +2712,7 @@ uint32_t mro_scenario_from_name(const char* name) {
 int mro_cfg_init(mr_cfg* c, uint32_t scn) {
   static const uint8_t k_n[MR_SCN_COUNT_] = {0, 3, 3, 7, 5, 3, 5, 3, 3, 5, 3, 3, 5, 3,
                                              5, 5, 5, 5, 5, 3, 3, 3, 3, 3, 5, 5, 5, 5, 3, 3,
-                                             5, 5, 5, 5, 5, 5, 5, 3, 5, 3, 3, 5, 5, 5, 5, 5};
+                                             5, 5, 5, 5, 5, 5, 5, 3, 5, 3, 3, 5, 5, 5, 5, 5, 7, 7};
   if (scn == 0 || scn >= MR_SCN_COUNT_) return -1;
   memset(c, 0, sizeof *c);
   c->abi_version = MR_ABI_VERSION;
@@ -2615,7 +2730,7 @@ int mro_cfg_init(mr_cfg* c, uint32_t scn) {
                : churn ? 4096 : scn == MR_SCN_UNRELIABLE_AGREE_2C ? 1024 : 0;
   c->log_cap = cap ? cap : 256;
   c->apply_cap = cap ? cap : (snap ? 1024 : 512);
-  c->msg_slots = scn == MR_SCN_KV_SNAPSHOT_RECOVER_MANY_CLIENTS_3B ? 256 : kv ? 64 : 32;
+  c->msg_slots = mr_scn_wide_slots(scn) ? 256 : kv ? 64 : 32;
   c->ae_max = 16;
   c->hb_us = 50000;
   c->elect_lo_us = 150000;

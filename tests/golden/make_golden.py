@@ -32,6 +32,13 @@ CASES += [
          first=0, count=8),
     dict(test="rejoin_2b", cfg={"flags": _abi.MR_F_SAFETY | _abi.MR_F_BUG_NO_PREV_CHECK},
          first=0, count=8),
+    # generic_test_linearizability's checker (SEMANTICS §9b) and the buggy servers it catches
+    dict(test="persist_partition_unreliable_linearizable_3a", cfg={"flags": _abi.MR_F_BUG_NO_DEDUP},
+         first=0, count=4),
+    dict(test="persist_partition_unreliable_linearizable_3a",
+         cfg={"flags": _abi.MR_F_BUG_STALE_READ}, first=0, count=8),
+    dict(test="snapshot_unreliable_recover_concurrent_partition_linearizable_3b",
+         cfg={"flags": _abi.MR_F_BUG_NO_DEDUP}, first=0, count=4),
 ]
 
 

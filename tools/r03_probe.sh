@@ -17,7 +17,3 @@ timeout -s KILL 60 rocprofv3 --pmc TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum --ker
 cat $O/sc_f.log $O/st_f.log
 timeout -k 10 400 python bench.py --steps 5 --warmup 2 > $O/bench.json 2> $O/bench.err || { echo "bench failed"; exit 1; }
 cat $O/bench.json
-bash tools/r03_ab1.sh || exit 1
-LIB=pcs bash tools/r03_pcs.sh || exit 1
-mv gpurun_out/r03pcs gpurun_out/r03pcs_old
-LIB=pcs1 bash tools/r03_pcs.sh || exit 1
