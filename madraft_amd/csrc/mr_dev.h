@@ -198,6 +198,10 @@ struct Dev {
   uint32_t lpw;         // lanes of each 64-lane block that hold a cluster (64, 32, 16; the rest idle)
   uint32_t c0;          // first cluster of this launch's chunk
   uint32_t stream;      // MR_F_STREAM: a lane that finishes takes the next unclaimed cluster
+  uint32_t resume;      // streaming, not the chunk's first launch: lanes first take held_in[]
+  uint32_t nheld;       // ... the clusters the previous launch's lanes still held
+  uint32_t* held_in;    // [L] those clusters (streaming)
+  uint32_t* held_out;   // [L] this launch's (index = its remaining[0] count)
   unsigned long long* prof;  // [PROF_SLOTS] wave-cycle profile (MR_PROF builds only)
 };
 constexpr uint32_t PROF_SLOTS = 64;

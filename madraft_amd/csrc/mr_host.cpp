@@ -109,6 +109,9 @@ struct mr_batch {
   uint32_t* h_remaining = nullptr;  // [2]: remaining, next unclaimed cluster (D.remaining)
   uint32_t* h_ctl0 = nullptr;       // [2]: {0, L}, copied to D.remaining before each launch
   uint32_t c_open = 0;              // first cluster of the first chunk not yet finished
+  uint32_t* held[2] = {nullptr, nullptr};  // streaming: clusters held at a launch's end (ping-pong)
+  uint32_t hsel = 0;                // held[hsel] = the next launch's held_in
+  bool resume = false;              // streaming: the next launch continues the current chunk
   hipStream_t stream = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   uint32_t budget = 16384;  // events per cluster per launch (MR_STEP_BUDGET)
@@ -347,6 +350,14 @@ static int mr_batch_create_impl(const mr_cfg* cfg, mr_batch** out) {
     *it.p = it.bytes ? p : nullptr;
     p += (it.bytes + 255) & ~size_t(255);
   }
+  if (b->D.stream) {  // held-cluster lists, L entries each (L <= C)
+    e = hipMalloc(&b->held[0], (size_t)b->D.C * sizeof(uint32_t));
+    if (e == hipSuccess) e = hipMalloc(&b->held[1], (size_t)b->D.C * sizeof(uint32_t));
+    if (e != hipSuccess) {
+      mr_batch_destroy(b);
+      return set_err(std::string("held-list allocation failed: ") + hipGetErrorString(e));
+    }
+  }
   if (cfg->flags & MR_F_RECORD) {
     e = hipMalloc(&b->tape, (size_t)C * cfg->tape_cap * sizeof(uint4));
     if (e != hipSuccess) {
@@ -385,6 +396,7 @@ static int mr_batch_create_impl(const mr_cfg* cfg, mr_batch** out) {
 static int enqueue_reset(mr_batch* b, uint64_t seed_base) {
   b->cfg.seed_base = seed_base;
   b->c_open = 0;
+  b->resume = false;
   b->D.seed0 = seed_base + b->cfg.cluster_base;
   HIPCHK(hipSetDevice(b->cfg.device));
   HIPCHK(hipMemsetAsync(b->D.stor, 0, (size_t)b->D.C * b->D.apply_cap * sizeof(SE), b->stream));
@@ -407,7 +419,19 @@ static int enqueue_reset(mr_batch* b, uint64_t seed_base) {
 // the remaining-cluster count is copied back asynchronously
 static int enqueue_step(mr_batch* b, uint32_t budget) {
   b->h_ctl0[0] = 0;
-  b->h_ctl0[1] = b->D.c0 + b->D.L;  // lanes start with clusters c0 .. c0+L-1 (streaming: claim on)
+  if (b->D.stream && b->resume) {  // continue: the held clusters first, the claim pointer kept
+    b->h_ctl0[1] = b->h_remaining[1];
+    b->D.nheld = b->h_remaining[0];
+    b->D.resume = 1;
+  } else {
+    b->h_ctl0[1] = b->D.c0 + b->D.L;  // lanes start with clusters c0 .. c0+L-1 (streaming: claim on)
+    b->D.nheld = 0;
+    b->D.resume = 0;
+  }
+  b->D.held_in = b->held[b->hsel];
+  b->D.held_out = b->held[b->hsel ^ 1u];
+  b->hsel ^= 1u;
+  b->resume = b->D.stream != 0;
   HIPCHK(hipMemcpyAsync(b->D.remaining, b->h_ctl0, 2 * sizeof(uint32_t), hipMemcpyHostToDevice,
                         b->stream));
   HIPCHK(hipEventRecord(b->ev0, b->stream));
@@ -611,6 +635,8 @@ uint32_t mr_decision_word(uint32_t v, uint32_t lo, uint32_t hi) {
 static void drop_decisions(mr_batch* b) {
   if (b->tape) (void)hipFree(b->tape);
   if (b->doff) (void)hipFree(b->doff);
+  if (b->held[0]) (void)hipFree(b->held[0]);
+  if (b->held[1]) (void)hipFree(b->held[1]);
   b->tape = nullptr;
   b->doff = nullptr;
   b->D.dtab = nullptr; b->D.doff = nullptr; b->D.dcap = 0; b->D.tape_mode = 0;

@@ -110,6 +110,12 @@ constexpr uint32_t STEP_BLOCK = MW > 2 ? 64 : MR_BLOCK;
 #ifndef MR_AE_K0  // heartbeats (no entries) in the AE sub-class too
 #define MR_AE_K0 1
 #endif
+#ifndef MR_AE_KMIN  // A/B: only AppendEntries with at least this many entries in the sub-class
+#define MR_AE_KMIN 0
+#endif
+#ifndef MR_AE_OTHERS  // A/B: defer only while at least this many other node events run
+#define MR_AE_OTHERS 0
+#endif
 #ifndef MR_HB_CLASS  // leaders' heartbeat timers as a sub-class of their own (same rule)
 #define MR_HB_CLASS 0
 #endif
@@ -543,7 +549,7 @@ DI int net_send(const Dev& D, X& x, uint32_t src, uint32_t& nctr, uint32_t dst, 
     // bit 5: AppendEntries request (the step loop's AE sub-class, MR_AE_CLASS); below the
     // unique seq, so it never decides the order
     const uint64_t key = ((uint64_t)t << 32) | (seq << 6) |
-                         (type == M_AE_REQ && (MR_AE_K0 || k) ? 32u : 0u) | dst;
+                         (type == M_AE_REQ && (MR_AE_K0 || k) && k >= MR_AE_KMIN ? 32u : 0u) | dst;
     LK(slot) = key;
     if (key < x.mmin) { x.mmin = key; x.mslot = slot; }
   }
@@ -1678,11 +1684,11 @@ DI void tester(const Dev& D, X& x) {
       if constexpr (is_svc(S)) {
         done = t.helper == H_CALL ? call_step(D, x, t) : join_step(D, x, t);
       } else if constexpr (nthr(S) > 0) {
-        done = t.helper == H_ONE    ? one_step(D, x, t)
+        done = t.helper == H_ONE    ? one_step(D, x, t, true)
                : t.helper == H_WAIT ? wait_step(D, x, t)
                                     : join_step(D, x, t);  // H_JOIN: join_all
       } else {
-        done = t.helper == H_ONE   ? one_step(D, x, t)
+        done = t.helper == H_ONE   ? one_step(D, x, t, true)
                : t.helper == H_COL ? col_step(D, x, t)
                                    : wait_step(D, x, t);
       }
@@ -1796,19 +1802,26 @@ __global__ void __launch_bounds__(STEP_BLOCK, step_waves<S>()) step_kernel(Dev D
   X x;
   // lanes 0 .. lpw - 1 of each 64-lane block hold clusters (D.lpw < 64: a batch smaller than the
   // resident lanes still spreads over two waves per SIMD; the other lanes idle)
-  x.c = blockIdx.x * D.lpw + threadIdx.x;
+  x.c = blockIdx.x * D.lpw + threadIdx.x;  // this launch's lane
 #ifdef MR_PROF
   if ((threadIdx.x & 63) == 0) {
     for (uint32_t k = 0; k < 2 * P__N; k++) s_prof[threadIdx.x >> 6][k] = 0;
     s_prof[threadIdx.x >> 6][2 * P__N] = wall_clock64();
   }
 #endif
-  x.c += D.c0;  // lane l starts with cluster c0 + l of this launch's chunk
-  const bool in = threadIdx.x < D.lpw && x.c < D.c0 + D.L && x.c < D.C;
+  const bool lane_ok = threadIdx.x < D.lpw && x.c < D.L;
+  bool in;
+  if (D.stream && D.resume) {  // a later launch of a streaming batch: the clusters the previous
+    in = lane_ok && x.c < D.nheld;  // launch's lanes still held first, then the claim pointer
+    if (in) x.c = D.held_in[x.c];
+  } else {
+    x.c += D.c0;  // lane l starts with cluster c0 + l of this launch's chunk
+    in = lane_ok && x.c < D.C;
+  }
   x.code = MR_PASS;
   if (in) lane_load<S>(D, x);
   bool held = x.code == RUN;  // this lane runs cluster x.c (its state is in registers / LDS)
-  if (D.stream) held = held || lane_claim<S>(D, x, in && !held);
+  if (D.stream) held = held || lane_claim<S>(D, x, (D.resume ? lane_ok : in) && !held);
   PROF(P_PRO);
   uint64_t key = 0;
   uint32_t cls = CLS_NONE, node = 0;
@@ -1870,7 +1883,9 @@ __global__ void __launch_bounds__(STEP_BLOCK, step_waves<S>()) step_kernel(Dev D
       if (!tpick) {
         const bool ae = run && cls == CLS_MSG && ((key >> 5) & 1u);
         const uint32_t nae = __popcll(__ballot(ae));
-        if (nae < nm + nt && MR_AE_DEN * nae < MR_AE_NUM * (nm + nt)) mine = mine && !ae;
+        if (nae < nm + nt && MR_AE_DEN * nae < MR_AE_NUM * (nm + nt) &&
+            nm + nt - nae >= MR_AE_OTHERS)
+          mine = mine && !ae;
         if constexpr (MR_HB_CLASS) {
           const bool hb = run && cls == CLS_TIMER && bit(x.lmask, node);
           const uint32_t nhb = __popcll(__ballot(hb));
@@ -1916,7 +1931,10 @@ __global__ void __launch_bounds__(STEP_BLOCK, step_waves<S>()) step_kernel(Dev D
 #endif
   if (!held) return;
   lane_store<S>(D, x);
-  if (x.code == RUN) atomicAdd(D.remaining, 1u);
+  if (x.code == RUN) {  // still running: counted, and (streaming) resumed first by the next launch
+    const uint32_t k = atomicAdd(D.remaining, 1u);
+    if (D.stream) D.held_out[k] = x.c;
+  }
 }
 
 #ifndef MR_COMMON

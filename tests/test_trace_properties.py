@@ -1,0 +1,88 @@
+"""Raft properties read straight off the event traces — a check that does not go through the
+oracle. Parity (tests/test_gpu_parity.py) shows the GPU and the oracle agree; both restate one
+docs/SEMANTICS.md, so a misreading common to both would pass it. These properties come from the
+Raft paper (Figure 3) and the trace format alone (SEMANTICS §7: after every node event, the
+node's role / term / commit / applied / last / snapshot index), and hold for any correct Raft:
+
+* times never go back; a node's term never decreases (it is persisted across crashes);
+* election safety: at most one node is leader in a term;
+* snapshot <= applied <= commit <= last on a live node;
+* without crashes, a node's commit and applied indices never decrease, and its snapshot index
+  never decreases either way.
+
+CPU: oracle traces of many seeds over the BASELINE shapes; GPU: the HIP path's own traces.
+"""
+import numpy as np
+import pytest
+
+from madraft_amd import _abi
+
+R_L, R_DOWN = 2, 3
+NO_CRASH = {"figure_8_unreliable_2c", "fail_agree_2b", "basic_agree_2b", "unreliable_3a",
+            "snapshot_install_unreliable_2d", "many_partitions_many_clients_3a"}
+
+
+def check_trace(tr, test):
+    assert (np.diff(tr["time_us"].astype(np.int64)) >= 0).all(), "time went back"
+    node = tr[(tr["cls"] <= 1) & (tr["node"] < 8)]  # node events (messages, timers)
+    leaders = {}
+    for d in np.unique(node["node"]):
+        r = node[node["node"] == d]
+        assert (np.diff(r["term"].astype(np.int64)) >= 0).all(), f"node {d}: term decreased"
+        live = r[r["role"] != R_DOWN]
+        assert (live["snap"] <= live["applied"]).all(), f"node {d}: applied below the snapshot"
+        assert (live["applied"] <= live["commit"]).all(), f"node {d}: applied beyond commit"
+        assert (live["commit"] <= live["last"]).all(), f"node {d}: commit beyond the log"
+        assert (np.diff(r["snap"].astype(np.int64)) >= 0).all(), f"node {d}: snapshot went back"
+        if test in NO_CRASH:
+            assert (np.diff(r["commit"].astype(np.int64)) >= 0).all(), f"node {d}: commit went back"
+            assert (np.diff(r["applied"].astype(np.int64)) >= 0).all(), f"node {d}: applied went back"
+        for t in np.unique(r["term"][r["role"] == R_L]):
+            assert leaders.setdefault(int(t), int(d)) == int(d), f"two leaders in term {t}"
+    return len(leaders)
+
+
+CASES = [("figure_8_unreliable_2c", {}), ("figure_8_unreliable_crash", {}),
+         ("fail_agree_2b", dict(n_nodes=5, flags=_abi.MR_F_UNRELIABLE)),
+         ("snapshot_install_unreliable_2d", dict(n_nodes=7)), ("unreliable_3a", {}),
+         ("persist_partition_unreliable_linearizable_3a", {}), ("unreliable_churn_2c", {})]
+
+
+@pytest.mark.parametrize("test,kw", CASES)
+def test_oracle_traces_hold_raft_properties(oracle, test, kw):
+    terms = 0
+    for c in range(24):
+        cfg = oracle.cfg(test, **kw)
+        r, tr = oracle.run_cluster(cfg, c, trace_cap=1 << 17)
+        assert tr[-1]["cls"] == 3 and tr[-1]["kind"] == r["code"], "trace truncated"
+        terms += check_trace(tr, test)
+    assert terms > 24  # leaders were elected: the properties had something to hold for
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("test,kw", CASES)
+def test_gpu_traces_hold_raft_properties(hip, test, kw):
+    kw = {("nodes" if k == "n_nodes" else k): v for k, v in kw.items()}
+    if "flags" in kw and kw["flags"] & _abi.MR_F_UNRELIABLE:
+        kw.pop("flags")
+        kw["unreliable"] = True
+    with hip.Batch(test, 64, trace_clusters=16, trace_cap=1 << 17, **kw) as b:
+        b.run()
+        traces = [b.trace(k) for k in range(16)]
+    assert all(tr[-1]["cls"] == 3 for tr in traces)  # complete: each ends with its verdict
+    assert sum(check_trace(tr, test) for tr in traces) > 16
+
+
+@pytest.mark.parametrize("test,bug", [("many_election_2a", _abi.MR_F_BUG_VOTE_TWICE),
+                                      ("figure_8_unreliable_2c", _abi.MR_F_BUG_VOTE_STALE)])
+def test_trace_properties_catch_buggy_raft(oracle, test, bug):
+    """The trace checks are not vacuous: a Raft that votes twice in a term (or for a stale
+    log) elects two leaders in one term on some seeds, and the trace alone shows it."""
+    caught = 0
+    for c in range(64):
+        _, tr = oracle.run_cluster(oracle.cfg(test, flags=bug), c, trace_cap=1 << 17)
+        try:
+            check_trace(tr, test)
+        except AssertionError:
+            caught += 1
+    assert caught >= 1

@@ -2,11 +2,13 @@
 
 usage: python tools/pmc_sum.py <pmc_dir> [--json out.json --test T --clusters C]
 
-HBM bytes follow MI355X_MICROARCH.md §HBM: FETCH_SIZE and WRITE_SIZE are in
-KiB; FETCH_SIZE is scaled by --fetch-factor (the guide's 2 for wide coalesced
-streaming reads; DESIGN.md §6.2 records what tools/memlat.hip measured for this
-kernel's scattered record reads). With --json the per-launch traffic is written in
-the form bench.py's roofline.traffic reads (profiles/pmc_*.json), stamped with the
+HBM traffic per launch, from the L2's fabric request counters (one pass per counter group):
+reads = 128 x TCC_EA0_RDREQ_128B + 64 x _64B + 32 x _32B, writes = 64 x TCC_EA0_WRREQ_64B +
+32 x (TCC_EA0_WRREQ - _64B). profiles/r03_fetch_calibration.txt: every read request of the
+step kernel's shapes (scattered 16-B records and coalesced words) is a whole 128-B line, and
+FETCH_SIZE (= RDREQ x 64 B) undercounts it by exactly 2 — the MI355X_MICROARCH.md doubling —
+so FETCH_SIZE x 2 + WRITE_SIZE is printed beside it as a cross-check. With --json the record
+bench.py's roofline.traffic reads (profiles/pmc_*.json) is written, stamped with the
 lib_sha16 the profiled bench runs printed: bench.py uses a record only for that build.
 """
 import argparse
@@ -20,25 +22,25 @@ ap.add_argument("dir")
 ap.add_argument("--json")
 ap.add_argument("--test", default="figure_8_unreliable_2c")
 ap.add_argument("--clusters", type=int, default=131072)
-ap.add_argument("--fetch-factor", type=float, default=2.0)
 a = ap.parse_args()
 
 agg = collections.defaultdict(float)
 disp = {}
 for p in sorted(glob.glob(f"{a.dir}/p*/run_counter_collection.csv")):
-    ids = set()
+    ids, names = set(), set()
     for r in csv.DictReader(open(p)):
         if "step_kernel" not in r["Kernel_Name"]:
             continue
         agg[r["Counter_Name"]] += float(r["Counter_Value"])
         ids.add(r["Dispatch_Id"])
-    for k in {r for r in agg}:
-        disp.setdefault(k, len(ids))
+        names.add(r["Counter_Name"])
+    for k in names:
+        disp[k] = len(ids)
 nd = max(disp.values()) if disp else 0
 wc = agg.get("SQ_WAVE_CYCLES", 1)
 print(f"dispatches={nd}")
 for k in sorted(agg):
-    print(f"{k:28s} {agg[k]:.4g}")
+    print(f"{k:32s} {agg[k]:.4g}")
 if "SQ_WAIT_ANY" in agg:
     print(f"wait_any/wave_cycles = {agg['SQ_WAIT_ANY'] / wc:.3f}  "
           f"active/wave_cycles = {agg['SQ_ACTIVE_INST_ANY'] / wc:.3f}")
@@ -54,20 +56,34 @@ if len(libs) > 1:
     raise SystemExit(f"PMC passes of different library builds: {sorted(libs)}")
 lib = libs.pop() if libs else None
 print(f"lib_sha16={lib}")
-if "FETCH_SIZE" in agg:
-    rd = a.fetch_factor * agg["FETCH_SIZE"] * 1024
-    wr = agg.get("WRITE_SIZE", 0) * 1024
-    per = (rd + wr) / max(disp.get("FETCH_SIZE", nd), 1)
-    print(f"HBM bytes ({a.fetch_factor:g}*FETCH_SIZE + WRITE_SIZE, KiB->B) = {rd + wr:.4g}; "
-          f"per launch {per:.4g}")
-    if a.json:
-        if lib is None:
-            raise SystemExit("no lib_sha16 in the bench logs: cannot stamp the record")
-        json.dump({"test": a.test, "clusters": a.clusters, "kernel": "step_kernel", "abi": 3,
-                   "lib_sha16": lib, "fetch_factor": a.fetch_factor,
-                   "dispatches": disp.get("FETCH_SIZE", nd), "hbm_read_bytes": rd,
-                   "hbm_write_bytes": wr, "hbm_bytes_per_launch": per,
-                   "counters": dict(agg),
-                   "method": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE in separate passes; "
-                             f"FETCH_SIZE x {a.fetch_factor:g} (DESIGN.md 6.2)"},
-                  open(a.json, "w"), indent=1)
+
+
+def per_launch(name):
+    return agg[name] / max(disp.get(name, nd), 1)
+
+
+out = {"test": a.test, "clusters": a.clusters, "kernel": "step_kernel", "abi": 3, "lib_sha16": lib,
+       "counters": dict(agg), "dispatches": disp}
+if "FETCH_SIZE" in agg and "WRITE_SIZE" in agg:
+    fs = 2 * per_launch("FETCH_SIZE") * 1024 + per_launch("WRITE_SIZE") * 1024
+    out["fetch2_write_bytes_per_launch"] = fs
+    print(f"2 x FETCH_SIZE + WRITE_SIZE per launch = {fs:.4g} B")
+req = ("TCC_EA0_RDREQ_128B_sum", "TCC_EA0_RDREQ_64B_sum", "TCC_EA0_WRREQ_sum", "TCC_EA0_WRREQ_64B_sum")
+if all(k in agg for k in req):
+    rd = (128 * per_launch("TCC_EA0_RDREQ_128B_sum") + 64 * per_launch("TCC_EA0_RDREQ_64B_sum")
+          + 32 * (per_launch("TCC_EA0_RDREQ_32B_sum") if "TCC_EA0_RDREQ_32B_sum" in agg else 0))
+    w64 = per_launch("TCC_EA0_WRREQ_64B_sum")
+    wr = 64 * w64 + 32 * (per_launch("TCC_EA0_WRREQ_sum") - w64)
+    out.update(hbm_read_bytes=rd, hbm_write_bytes=wr, hbm_bytes_per_launch=rd + wr,
+               method="rocprofv3 --pmc, one pass per group: reads 128/64/32 x TCC_EA0_RDREQ_"
+                      "{128B,64B,32B}, writes 64 x WRREQ_64B + 32 x the rest (DESIGN.md 6.2)")
+    print(f"request-size HBM bytes per launch: read {rd:.4g} + write {wr:.4g} = {rd + wr:.4g}")
+elif "fetch2_write_bytes_per_launch" in out:
+    out.update(hbm_bytes_per_launch=out["fetch2_write_bytes_per_launch"],
+               method="rocprofv3 --pmc FETCH_SIZE x 2 + WRITE_SIZE (profiles/r03_fetch_calibration.txt)")
+if a.json:
+    if lib is None:
+        raise SystemExit("no lib_sha16 in the bench logs: cannot stamp the record")
+    if "hbm_bytes_per_launch" not in out:
+        raise SystemExit("no traffic counters in these passes")
+    json.dump(out, open(a.json, "w"), indent=1)
