@@ -285,6 +285,13 @@ constexpr bool has_nb7(uint32_t s) {
 constexpr bool uses_service_snapshots(uint32_t s) {
   return s >= MR_SCN_SNAPSHOT_BASIC_2D && s <= MR_SCN_SNAPSHOT_INSTALL_UNRELIABLE_CRASH_2D;
 }
+// test bodies that crash and restart servers (crash1 / start1, tester.rs:293-333): persist1-3,
+// figure_8 and its unreliable crash variant, the 2D crash variants, the churn tests
+constexpr bool restarts_servers(uint32_t s) {
+  return (s >= MR_SCN_PERSIST1_2C && s <= MR_SCN_FIGURE_8_2C) || s == MR_SCN_RELIABLE_CHURN_2C ||
+         s == MR_SCN_UNRELIABLE_CHURN_2C || s == MR_SCN_SNAPSHOT_INSTALL_CRASH_2D ||
+         s == MR_SCN_SNAPSHOT_INSTALL_UNRELIABLE_CRASH_2D || s == MR_SCN_FIGURE_8_UNRELIABLE_CRASH;
+}
 #define MR_ALL_SCNS                                                                       \
   MR_INST(1) MR_INST(2) MR_INST(3) MR_INST(4) MR_INST(5) MR_INST(6) MR_INST(7) MR_INST(8) \
   MR_INST(9) MR_INST(10) MR_INST(11) MR_INST(12) MR_INST(13) MR_INST(14) MR_INST(16)      \

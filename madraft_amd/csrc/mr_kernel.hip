@@ -97,9 +97,11 @@ constexpr uint32_t STEP_BLOCK = MW > 2 ? 64 : MR_BLOCK;
 #ifndef MR_KEY32
 #define MR_KEY32 0
 #endif
-// AppendEntries deliveries as a sub-class of the node events (step_kernel), a scheduling
-// policy chosen per scenario by A/B (profiles/r02_ab_configs.txt): figure_8_unreliable_2c
-// +6.5 %; its crash variant -8.5 %, kvraft unreliable_3a -6.7 %, fail_agree_2b 0: off there
+// AppendEntries deliveries as a sub-class of the node events (step_kernel): a scheduling policy
+// (results do not depend on it) for the Raft-only kernels with 64-bit keys whose test body does
+// not restart servers (restarts_servers, mr_dev.h). A/B (profiles/r03_ab_round3.txt):
+// figure_8_unreliable_2c +6.5 %, fail_agree_2b 0; with restarts (figure_8_unreliable_crash) -9 %
+// and in the kvraft kernels (unreliable_3a) -7 %, for every per-wave threshold tried
 #ifndef MR_AE_CLASS
 #define MR_AE_CLASS 1
 #endif
@@ -113,8 +115,8 @@ constexpr uint32_t STEP_BLOCK = MW > 2 ? 64 : MR_BLOCK;
 #ifndef MR_AE_KMIN  // A/B: only AppendEntries with at least this many entries in the sub-class
 #define MR_AE_KMIN 0
 #endif
-#ifndef MR_AE_OTHERS  // A/B: defer only while at least this many other node events run
-#define MR_AE_OTHERS 0
+#ifndef MR_AE_OTHERS  // defer only while at least this many other node events run (A/B: 0
+#define MR_AE_OTHERS 32  // 132.4, 32 131.65, 40 134.9, 48 139.75 ms on figure_8_unreliable_2c)
 #endif
 #ifndef MR_HB_CLASS  // leaders' heartbeat timers as a sub-class of their own (same rule)
 #define MR_HB_CLASS 0
@@ -370,9 +372,7 @@ __device__ __forceinline__ uint64_t fnv8(uint64_t h, uint32_t w0, uint32_t w1, u
 }
 DI void rec8(const Dev& D, X& x, uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3, uint32_t w4,
              uint32_t w5, uint32_t w6, uint32_t w7) {
-#ifndef MR_DEV_NO_DIGEST  // timing experiments only: NOT the simulator (breaks the digest)
   x.digest = fnv8(x.digest, w0, w1, w2, w3, w4, w5, w6, w7);
-#endif
   if (x.c < D.trace_clusters && x.trace_n < D.trace_cap) {
     uint32_t* p = reinterpret_cast<uint32_t*>(D.trace + (size_t)x.c * D.trace_cap + x.trace_n);
     p[0] = w0; p[1] = w1; p[2] = w2; p[3] = w3; p[4] = w4; p[5] = w5; p[6] = w6; p[7] = w7;
@@ -1664,18 +1664,6 @@ DI void tester(const Dev& D, X& x) {
 #pragma unroll
   for (uint32_t k = 0; k < T_NH; k++) t.h[k] = CS(CS_TH + k);
   t.hv = C64(C64_THV);
-#ifndef MR_T_PREFETCH  // A/B: the leader's record fetched with the frame (figure_8 start() loop)
-#define MR_T_PREFETCH 0
-#endif
-  if constexpr (MR_T_PREFETCH && (S == MR_SCN_FIGURE_8_UNRELIABLE_2C || S == MR_SCN_FIGURE_8_2C ||
-                                  S == MR_SCN_FIGURE_8_UNRELIABLE_CRASH)) {
-    // the record of the lowest leader: its first 64 B (scalars, pending payload range) reach
-    // the cache with the frame's loads, so start() on it waits for a cache hit, not HBM
-    if (x.lmask) {
-      const uint32_t pf = ND(NF_FLAGS, (uint32_t)__builtin_ctz(x.lmask));
-      asm volatile("" ::"v"(pf));
-    }
-  }
   x.yield = 0;
   for (int guard = 0;; guard++) {
     if (guard > 4096) { fail(D, x, MR_FAIL_SIM_BAD_PROGRAM); return; }
@@ -1879,7 +1867,7 @@ __global__ void __launch_bounds__(STEP_BLOCK, step_waves<S>()) step_kernel(Dev D
 #ifndef MR_AE_ALL  // A/B: the AppendEntries sub-class for every 64-bit-key scenario
 #define MR_AE_ALL 0
 #endif
-    if constexpr (MR_AE_CLASS && !MR_KEY32 && (MR_AE_ALL || S == MR_SCN_FIGURE_8_UNRELIABLE_2C)) {
+    if constexpr (MR_AE_CLASS && !MR_KEY32 && (MR_AE_ALL || (!is_svc(S) && !restarts_servers(S)))) {
       if (!tpick) {
         const bool ae = run && cls == CLS_MSG && ((key >> 5) & 1u);
         const uint32_t nae = __popcll(__ballot(ae));

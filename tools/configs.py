@@ -16,7 +16,7 @@ import torch  # noqa: F401  (HIP runtime first)
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))  # repo root
 from madraft_amd import _abi, sim
 
-ROOT = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 EXE = os.path.join(ROOT, "oracle", "_build", "mr_oracle")
 CPU_S = float(sys.argv[1]) if len(sys.argv) > 1 else 6.0
 
@@ -31,6 +31,10 @@ CONFIGS = [  # (name, test, clusters per GPU, Batch kwargs, oracle CLI args)
     ("C4 snapshot_install_unreliable_2d, 7 nodes", "snapshot_install_unreliable_2d", 262144,
      dict(nodes=7), ["--nodes", "7"]),
     ("C5 unreliable_3a kvraft, 5 servers + 5 clerks", "unreliable_3a", 65536, {}, []),
+    ("C5-lin persist_partition_unreliable_linearizable_3a, 7 servers + 15 clerks",
+     "persist_partition_unreliable_linearizable_3a", 65536, {}, []),
+    ("C5-lin snapshot_..._concurrent_partition_linearizable_3b, 7 servers + 15 clerks",
+     "snapshot_unreliable_recover_concurrent_partition_linearizable_3b", 65536, {}, []),
 ]
 
 
@@ -65,6 +69,7 @@ for name, test, c, kw, args in CONFIGS:
         cnt = b.counters()
     cs, ce, n = cpu_rate(test, args, CPU_S)
     print(f"{name}: GPU {2 * c / wall:,.0f} seeds/s, {ev / wall / 1e9:.3f} G events/s, "
-          f"{ms / 2:.1f} kernel ms per {c} clusters, pass {cnt['passed']}/{cnt['done']} | "
+          f"{ms / 2:.1f} kernel ms per {c} clusters, pass {cnt['passed']}/{cnt['done']}"
+          + (f", lin-checked Gets {cnt['kv_lin_checked']:,}" if cnt["kv_lin_checked"] else "") + " | "
           f"CPU (oracle, 16 procs, {n} seeds) {cs:,.0f} seeds/s, {ce / 1e6:.1f} M events/s | "
           f"x{2 * c / wall / cs:.1f}", flush=True)
