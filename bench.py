@@ -278,7 +278,7 @@ def main():
             "pass_rate": round(sv["passed"] / max(sv["done"], 1), 6),
             "note": "config 3 read literally: crash1/start1 + persister (tests.rs:612-660) in "
                     "figure_8_unreliable's loop"}}
-    if rank == 0 and not a.no_cpu_baseline:
+    if world == 1 and not a.no_cpu_baseline:  # N = 1 only: the N > 1 lines are scaling points
         # one process per host core this job may use (north_star): the CPUs it may run on, capped
         # by its cgroup CPU quota — on the GPU box 256 CPUs are visible but the quota is 16
         # cores, and 256 processes on 16 cores' time measured 38 % below 16 processes

@@ -1,10 +1,11 @@
 // Dev micro-benchmark (not product code): memory behaviour of the step kernel's access shapes
 // on one MI355X, to calibrate DESIGN.md §6.2's traffic / latency reading.
 //
-//   memlat chase <bytes_per_lane> <steps> <chains>
+//   memlat chase <bytes_per_lane> <steps> <chains> [lanes]
 //       every lane walks <chains> independent dependent-load chains through a private slice
-//       of <bytes_per_lane> bytes (random 16-B records), 131072 lanes in 64-lane blocks at
-//       two waves per SIMD (the step kernel's shape); prints ns per dependent round trip.
+//       of <bytes_per_lane> bytes (random 16-B records), <lanes> (default 131072) lanes in
+//       64-lane blocks at two waves per SIMD (the step kernel's shape); prints ns per dependent
+//       round trip. With few lanes the memory system is idle: the unloaded latency.
 //   memlat scatter16 <records_per_lane>
 //       every lane reads <records_per_lane> random 16-B records of an 8 GiB buffer (one
 //       128-B line each, no reuse): algorithmic bytes = lanes x records x 16, to compare
@@ -106,24 +107,26 @@ int main(int argc, char** argv) {
     const uint64_t bpl = std::strtoull(argv[2], nullptr, 10);
     const uint32_t steps = (uint32_t)std::atoi(argv[3]), ch = (uint32_t)std::atoi(argv[4]);
     const uint32_t recs = (uint32_t)(bpl / 16);
+    const uint32_t lanes = argc > 5 ? (uint32_t)std::atoi(argv[5]) : LANES;
+    if (lanes % 64 || lanes > LANES) { std::fprintf(stderr, "lanes: multiple of 64, <= %u\n", LANES); return 2; }
     uint4* buf;
-    CHK(hipMalloc(&buf, (size_t)LANES * recs * 16));
-    init_chase<<<LANES / 64, 64>>>(buf, recs);
+    CHK(hipMalloc(&buf, (size_t)lanes * recs * 16));
+    init_chase<<<lanes / 64, 64>>>(buf, recs);
     CHK(hipDeviceSynchronize());
     const size_t lds = 20 * 1024;  // the step kernel's 20 KiB per 64-lane block
     for (int rep = 0; rep < 2; rep++) {
       CHK(hipEventRecord(e0));
-      if (ch == 1) chase<1><<<LANES / 64, 64, lds>>>(buf, recs, steps, out);
-      else if (ch == 2) chase<2><<<LANES / 64, 64, lds>>>(buf, recs, steps, out);
-      else chase<4><<<LANES / 64, 64, lds>>>(buf, recs, steps, out);
+      if (ch == 1) chase<1><<<lanes / 64, 64, lds>>>(buf, recs, steps, out);
+      else if (ch == 2) chase<2><<<lanes / 64, 64, lds>>>(buf, recs, steps, out);
+      else chase<4><<<lanes / 64, 64, lds>>>(buf, recs, steps, out);
       CHK(hipEventRecord(e1));
       CHK(hipEventSynchronize(e1));
       CHK(hipEventElapsedTime(&ms, e0, e1));
     }
-    std::printf("chase bytes/lane=%llu footprint=%.2f GB steps=%u chains=%u: %.3f ms, %.1f ns per round trip, "
-                "%.1f G loads/s\n",
-                (unsigned long long)bpl, (double)LANES * bpl / 1e9, steps, ch, ms, ms * 1e6 / steps,
-                (double)LANES * steps * ch / (ms * 1e6));
+    std::printf("chase lanes=%u bytes/lane=%llu footprint=%.2f GB steps=%u chains=%u: %.3f ms, %.1f ns per round "
+                "trip, %.1f G loads/s\n",
+                lanes, (unsigned long long)bpl, (double)lanes * bpl / 1e9, steps, ch, ms, ms * 1e6 / steps,
+                (double)lanes * steps * ch / (ms * 1e6));
     CHK(hipFree(buf));
   } else if (!std::strcmp(mode, "scatter16")) {
     const uint32_t per = (uint32_t)std::atoi(argv[2]);
