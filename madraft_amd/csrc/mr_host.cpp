@@ -291,12 +291,9 @@ static int mr_batch_create_impl(const mr_cfg* cfg, mr_batch** out) {
   auto add = [&](auto** p, size_t count) {
     items.push_back({reinterpret_cast<void**>(p), count * sizeof(**p)});
   };
-  // the per-cluster scalar, node, timer and message arrays are addressed with 32-bit byte
-  // offsets in the kernels (mr_kernel.hip CS / C64 / NDP / TMR / MSP / MKEY)
+  // field matrices use 32-bit element offsets in the kernels
   const uint64_t lim = 1ull << 32;
-  if ((uint64_t)CS__N * C * 4 >= lim || (uint64_t)C64__N * C * 8 >= lim ||
-      (uint64_t)NREC * n * C * 4 >= lim || (uint64_t)MREC * M * C * 4 >= lim ||
-      (uint64_t)M * C * 8 >= lim) {
+  if ((uint64_t)CS__N * C >= lim || (uint64_t)C64__N * C >= lim || M * C >= lim) {
     delete b;
     return set_err("n_clusters too large for one batch (32-bit field offsets)");
   }
@@ -384,14 +381,6 @@ static int mr_batch_create_impl(const mr_cfg* cfg, mr_batch** out) {
   if (!cfg->lanes) {  // a batch bigger than the resident waves runs as chunks of that size
     const uint32_t capc = (uint32_t)((uint64_t)cap * b->D.lpw / STEP_LANES);
     if (capc && capc < b->D.C) b->D.L = capc;
-  }
-  {  // log / storage / payload offsets are 32-bit element offsets within one launch's clusters
-    const uint64_t span = b->D.stream ? b->D.C : b->D.L, lim = 1ull << 32;
-    if (span * n * cfg->log_cap >= lim || span * cfg->apply_cap >= lim || span * M * K >= lim) {
-      mr_batch_destroy(b);
-      return set_err("clusters per launch x log_cap (apply_cap, msg_slots x ae_max) must stay below "
-                     "2^32: lower mr_cfg.lanes, or turn MR_F_STREAM off");
-    }
   }
   if (const char* s = std::getenv("MR_STEP_BUDGET")) b->budget = (uint32_t)std::atoi(s);
   if (b->budget == 0) b->budget = 16384;

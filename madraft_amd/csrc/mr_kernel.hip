@@ -71,46 +71,18 @@ struct X {
 #endif
 };
 
-// field accessors: 32-bit BYTE offsets from the array's (kernel-argument, scalar) base, so
-// every access is one `global_load/store ... v_off, s[base]` with the field's word as the
-// immediate offset — no 64-bit address arithmetic per lane (the arrays' byte sizes are
-// checked below 2^32 at batch creation)
-#ifndef MR_OFF32
-#define MR_OFF32 1
-#endif
-#if MR_OFF32
-template <class T>
-DI T* at_b(T* base, uint32_t boff) {
-  return reinterpret_cast<T*>(reinterpret_cast<char*>(base) + boff);
-}
-#if MR_OFF32 == 2  // uniform field offset (scalar) + the lane's own byte offset
-#define CS(f) (*at_b(D.cs32, (uint32_t)(f) * (D.C * 4u) + x.c * 4u))
-#define C64(f) (*at_b(D.cs64, (uint32_t)(f) * (D.C * 8u) + x.c * 8u))
-#define MKEY(s) (*at_b(D.mkey, (uint32_t)(s) * (D.C * 8u) + x.c * 8u))
-#define TMR(d) (*at_b(D.tmr, (uint32_t)(d) * (D.C * 4u) + x.c * 4u))
-#define NDP(d) at_b(D.nd32, x.c * (D.n * NREC * 4u) + (uint32_t)(d) * (NREC * 4u))
-#define MSP(s) at_b(D.ms32, x.c * (D.M * MREC * 4u) + (uint32_t)(s) * (MREC * 4u))
-#else
-#define CS(f) (*at_b(D.cs32, ((uint32_t)(f) * D.C + x.c) * 4u))
-#define C64(f) (*at_b(D.cs64, ((uint32_t)(f) * D.C + x.c) * 8u))
-#define MKEY(s) (*at_b(D.mkey, ((uint32_t)(s) * D.C + x.c) * 8u))
-#define TMR(d) (*at_b(D.tmr, ((uint32_t)(d) * D.C + x.c) * 4u))
-#define NDP(d) at_b(D.nd32, (x.c * D.n + (uint32_t)(d)) * (NREC * 4u))  // node d's 128-B record
-#define MSP(s) at_b(D.ms32, (x.c * D.M + (uint32_t)(s)) * (MREC * 4u))  // message slot s's 32-B record
-#endif
-#else
+// field accessors (32-bit element offsets, checked at batch creation)
 #define CS(f) D.cs32[(uint32_t)(f) * D.C + x.c]
 #define C64(f) D.cs64[(uint32_t)(f) * D.C + x.c]
 #define NDP(d) (D.nd32 + ((size_t)x.c * D.n + (d)) * NREC)  // node d's 128-B record
-#define MSP(s) (D.ms32 + ((size_t)x.c * D.M + (s)) * MREC)  // message slot s's 32-B record
-#define MKEY(s) D.mkey[(size_t)(s) * D.C + x.c]
-#define TMR(d) D.tmr[(size_t)(d) * D.C + x.c]
-#endif
 #define ND(f, d) NDP(d)[f]
 #define NSV(d) (*reinterpret_cast<uint64_t*>(NDP(d) + NF_SNAPV))
 #define PR(f, d, p) NDP(d)[NR_PEER + (f) * MR_MAX_NODES + (p)]
+#define MSP(s) (D.ms32 + ((size_t)x.c * D.M + (s)) * MREC)  // message slot s's 32-B record
 #define MS32(f, s) MSP(s)[f]
 #define MSV(s) (*reinterpret_cast<uint64_t*>(MSP(s) + MF_V))
+#define MKEY(s) D.mkey[(size_t)(s) * D.C + x.c]
+#define TMR(d) D.tmr[(size_t)(d) * D.C + x.c]
 // message keys of the lane's cluster live in LDS during a launch: [slot][lane],
 // so a wave's 64 lanes read 64 consecutive u64 (conflict-free). Free slots hold
 // ~0, so the earliest-message scan is a branch-free min over all M slots.
@@ -295,24 +267,9 @@ DI void philox(const Dev& D, X& x, uint32_t c0, uint32_t c1, uint32_t c2, uint32
   w0 = w.x;
   w1 = w.y;
 }
-// The per-cluster log / storage / payload arrays as 32-bit element offsets from the launch
-// chunk's first cluster (MR_LOG32: step_kernel rebases D.log / D.stor / D.pay by D.c0; the host
-// checks chunk x n x log_cap etc. < 2^32): one 64-bit add per access instead of 64-bit products
-#ifndef MR_LOG32
-#define MR_LOG32 1
-#endif
-#if MR_LOG32
-using lix_t = uint32_t;
-#define LCL(c) ((c) - D.c0)
-#else
-using lix_t = size_t;
-#define LCL(c) ((size_t)(c))
-#endif
-DI lix_t logi(const Dev& D, const X& x, uint32_t d, uint32_t i) {
-  return (LCL(x.c) * D.n + d) * D.log_cap + (i & (D.log_cap - 1u));
+DI size_t logi(const Dev& D, const X& x, uint32_t d, uint32_t i) {
+  return ((size_t)x.c * D.n + d) * D.log_cap + (i & (D.log_cap - 1u));
 }
-#define STORI(c, j) (LCL(c) * D.apply_cap + (j))
-#define PAYP(s) (D.pay + (LCL(x.c) * D.M + (s)) * D.K)
 
 // One node's scalar state, loaded into registers at the start of an event
 // (one batch of independent loads) and stored back at its end.
@@ -643,7 +600,7 @@ DI void materialize(const Dev& D, X& x, uint32_t L, uint32_t& pexp) {
     const uint32_t hdr = MS32(MF_HDR, s), k = hdr_k(hdr);
     if (hdr_type(hdr) != M_AE_REQ || hdr_src(hdr) != L || (hdr & HDR_MAT) || k == 0) continue;
     const uint32_t prev = MS32(MF_A, s);
-    LE* pp = PAYP(s);
+    LE* pp = D.pay + ((size_t)x.c * D.M + s) * D.K;
     for (uint32_t j = 0; j < k; j++) pp[j] = D.log[logi(D, x, L, prev + 1 + j)];
     MS32(MF_HDR, s) = hdr | HDR_MAT;
     CADD(CNT_MATERIALIZED, k);
@@ -693,7 +650,7 @@ DI void storage_snapshot(const Dev& D, X& x, uint32_t i, uint32_t& slen, uint32_
   if (idx >= D.apply_cap) { fail(D, x, MR_FAIL_SIM_CAPACITY); return; }
   uint32_t nl = idx + 1;
   for (uint32_t j = nl; j < slen; j++) {
-    SE* e = D.stor + STORI(x.c, j);
+    SE* e = D.stor + (size_t)x.c * D.apply_cap + j;
     e->mask &= ~(1u << i);
   }
   slen = nl;
@@ -701,7 +658,7 @@ DI void storage_snapshot(const Dev& D, X& x, uint32_t i, uint32_t& slen, uint32_
 
 DI uint32_t n_committed(const Dev& D, X& x, uint32_t idx, uint64_t& v) {  // tester.rs:405-422
   if (idx >= D.apply_cap) { v = 0; return 0; }
-  const SE e = D.stor[STORI(x.c, idx)];
+  const SE e = D.stor[(size_t)x.c * D.apply_cap + idx];
   v = e.val;
   return (uint32_t)__builtin_popcount(e.mask);
 }
@@ -728,7 +685,7 @@ template <uint32_t S>
 DI void node_apply(const Dev& D, X& x, uint32_t me, NC& d, bool& kvready) {
   constexpr bool KV = is_svc(S);
   const bool snapmode = (x.netmode >> 1) & 1u;
-  SE* const sb = D.stor + STORI(x.c, 0u);
+  SE* const sb = D.stor + (size_t)x.c * D.apply_cap;
   uint32_t len = d.slen;
   uint32_t pm = 0;  // KV: the server's occupied pending-request slots (kv_apply)
   if constexpr (KV) pm = KVP(me)[KVR_PMASK];
@@ -961,8 +918,8 @@ DI void node_apply_coop(const Dev& D, X& x, uint32_t me, NC& d) {
     SE s = SE{};
     const bool inb = mine && i < D.apply_cap;
     if (inb) {
-      e = D.log[(LCL(oc) * D.n + ome) * D.log_cap + (i & (D.log_cap - 1u))];
-      s = D.stor[STORI(oc, i)];
+      e = D.log[((size_t)oc * D.n + ome) * D.log_cap + (i & (D.log_cap - 1u))];
+      s = D.stor[(size_t)oc * D.apply_cap + i];
     }
     uint32_t key = ~0u;
     if (mine) {
@@ -983,7 +940,7 @@ DI void node_apply_coop(const Dev& D, X& x, uint32_t me, NC& d) {
       const uint32_t fk = anyfail ? fkw[wave0 + o] : ~0u;
       const uint32_t f = fk == ~0u ? ~0u : fk >> 2;
       if (i < f && i >= olen)  // i == len in node_apply's walk: appended
-        D.stor[STORI(oc, i)] = SE{e.val, s.mask | (1u << ome), e.term};
+        D.stor[(size_t)oc * D.apply_cap + i] = SE{e.val, s.mask | (1u << ome), e.term};
       if (snapmode && i < f && (i + 1u) % 10u == 0u) {
         // the last snapshot index of the applied range [obase, min(oend, f - 1)]
         const uint32_t hi = f <= oend ? f - 1u : oend;
@@ -1056,7 +1013,7 @@ DI void safety_on_leader(const Dev& D, X& x, uint32_t me, const NC& d) {
   const uint32_t j = CNT_GET(CNT_MAX_INDEX);
   const uint32_t w = *lw;
   const LE le = D.log[logi(D, x, me, j)];
-  const SE se = D.stor[STORI(x.c, j)];
+  const SE se = D.stor[(size_t)x.c * D.apply_cap + j];
   if ((w >> (t & 31u)) & 1u) { fail(D, x, MR_FAIL_SAFETY_ELECTION); return; }
   *lw = w | (1u << (t & 31u));
   if (j > d.snap && (j > d.last || le.val != se.val || le.term != se.term))
@@ -1278,7 +1235,7 @@ DI void node_event(const Dev& D, X& x, bool is_msg, uint32_t tnode, uint32_t slo
           prev = d.snap; pterm = d.snapt;
         }
         if (prev > d.last) { rb = d.last + 1; break; }
-        const LE* pp = PAYP(slot);
+        const LE* pp = D.pay + ((size_t)x.c * D.M + slot) * D.K;
         const bool mat = (hdr_bits & HDR_MAT) != 0u;
         // one batch of independent loads: prev's term, then AC payload entries
         // (sender's ring or materialized copy) and our terms at their indices
@@ -1587,7 +1544,7 @@ DI bool t_start(const Dev& D, X& x, uint32_t i, uint64_t v, uint32_t& idx, uint3
   const uint32_t lrs = LRS(i);
   const uint32_t snap = r1.y, last = r1.x + 1;
   if (last - snap > D.log_cap) { fail(D, x, MR_FAIL_SIM_CAPACITY); return false; }
-  lix_t li = logi(D, x, i, last);
+  size_t li = logi(D, x, i, last);
   term = r0.y;
   uint32_t pexp = r2.y;
   const uint32_t rs = term == r2.w ? lrs : last;  // run start (le_at)
@@ -1830,11 +1787,6 @@ constexpr uint32_t step_waves() { return is_svc(S) ? 1u : (uint32_t)MR_WAVES_PER
 template <uint32_t S, uint32_t NBT>
 __global__ void __launch_bounds__(STEP_BLOCK, step_waves<S>()) step_kernel(Dev D, uint32_t budget) {
   static_assert(NBT == NB, "one node bound per translation unit");
-#if MR_LOG32
-  D.log += (size_t)D.c0 * D.n * D.log_cap;  // logi / STORI / PAYP offsets are chunk-relative
-  D.stor += (size_t)D.c0 * D.apply_cap;
-  D.pay += (size_t)D.c0 * D.M * D.K;
-#endif
   X x;
   // lanes 0 .. lpw - 1 of each 64-lane block hold clusters (D.lpw < 64: a batch smaller than the
   // resident lanes still spreads over two waves per SIMD; the other lanes idle)
@@ -1927,6 +1879,15 @@ __global__ void __launch_bounds__(STEP_BLOCK, step_waves<S>()) step_kernel(Dev D
           const uint32_t nhb = __popcll(__ballot(hb));
           if (nhb < nm + nt && MR_AE_DEN * nhb < MR_AE_NUM * (nm + nt)) mine = mine && !hb;
         }
+      }
+    }
+#ifndef MR_TCLI_CLASS  // spawned-thread steps and test-body steps as two sub-classes of the
+#define MR_TCLI_CLASS 0  // tester events: an iteration runs the larger group only
+#endif
+    if constexpr (MR_TCLI_CLASS && nthr(S) > 0) {
+      if (tpick) {
+        const uint32_t ncli = __popcll(__ballot(run && cls == CLS_TESTER && tcli));
+        if (ncli && ncli < ns) mine = mine && (tcli == (MR_TCLI_CLASS * ncli >= ns));
       }
     }
     PROF(P_SEL);
