@@ -1881,15 +1881,6 @@ __global__ void __launch_bounds__(STEP_BLOCK, step_waves<S>()) step_kernel(Dev D
         }
       }
     }
-#ifndef MR_TCLI_CLASS  // spawned-thread steps and test-body steps as two sub-classes of the
-#define MR_TCLI_CLASS 0  // tester events: an iteration runs the larger group only
-#endif
-    if constexpr (MR_TCLI_CLASS && nthr(S) > 0) {
-      if (tpick) {
-        const uint32_t ncli = __popcll(__ballot(run && cls == CLS_TESTER && tcli));
-        if (ncli && ncli < ns) mine = mine && (tcli == (MR_TCLI_CLASS * ncli >= ns));
-      }
-    }
     PROF(P_SEL);
     if (!run || !mine) continue;
     if (nthr(S) > 0 && (uint32_t)(key >> 32) == INF_T) {  // nothing can wake the test body
