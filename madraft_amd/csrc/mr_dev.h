@@ -285,6 +285,12 @@ constexpr bool has_nb7(uint32_t s) {
 constexpr bool uses_service_snapshots(uint32_t s) {
   return s >= MR_SCN_SNAPSHOT_BASIC_2D && s <= MR_SCN_SNAPSHOT_INSTALL_UNRELIABLE_CRASH_2D;
 }
+// scenarios in which a log can be compacted: the service snapshots of snap_common or a kvraft
+// maxraftstate. Everywhere else snap stays 0, so no InstallSnapshot is ever sent (the node
+// event compiles that path out of its send loop)
+constexpr bool has_snaps(uint32_t s) {
+  return uses_service_snapshots(s) || kv_gen(s).maxraft > 0;
+}
 // test bodies that crash and restart servers (crash1 / start1, tester.rs:293-333): persist1-3,
 // figure_8 and its unreliable crash variant, the 2D crash variants, the churn tests
 constexpr bool restarts_servers(uint32_t s) {

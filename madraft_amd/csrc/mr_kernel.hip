@@ -266,6 +266,14 @@ DI void philox(const Dev& D, X& x, uint32_t c0, uint32_t c1, uint32_t c2, uint32
   const uint2 w = philox2(c0, c1, c2, (uint32_t)seed, (uint32_t)(seed >> 32));
   w0 = w.x;
   w1 = w.y;
+#ifdef MR_DEV_DUP_PHILOX  // timing only: every draw computed twice (the copy's result is discarded)
+  {
+    uint32_t z = 0, k1 = (uint32_t)(seed >> 32) ^ 0x5bd1e995u;
+    asm volatile("" : "+v"(z), "+v"(k1));
+    const uint2 w2 = philox2(c0, c1, c2, (uint32_t)seed, k1);
+    w0 ^= (w2.x ^ w2.y) & z;
+  }
+#endif
 }
 DI size_t logi(const Dev& D, const X& x, uint32_t d, uint32_t i) {
   return ((size_t)x.c * D.n + d) * D.log_cap + (i & (D.log_cap - 1u));
@@ -373,6 +381,16 @@ __device__ __forceinline__ uint64_t fnv8(uint64_t h, uint32_t w0, uint32_t w1, u
 DI void rec8(const Dev& D, X& x, uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3, uint32_t w4,
              uint32_t w5, uint32_t w6, uint32_t w7) {
   x.digest = fnv8(x.digest, w0, w1, w2, w3, w4, w5, w6, w7);
+#ifdef MR_DEV_DUP_DIGEST  // timing only: the digest computed twice
+  {
+    uint64_t h2 = x.digest;
+    asm volatile("" : "+v"(h2));
+    h2 = fnv8(h2, w0, w1, w2, w3, w4, w5, w6, w7);
+    uint64_t z = 0;
+    asm volatile("" : "+v"(z));
+    x.digest ^= h2 & z;
+  }
+#endif
   if (x.c < D.trace_clusters && x.trace_n < D.trace_cap) {
     uint32_t* p = reinterpret_cast<uint32_t*>(D.trace + (size_t)x.c * D.trace_cap + x.trace_n);
     p[0] = w0; p[1] = w1; p[2] = w2; p[3] = w3; p[4] = w4; p[5] = w5; p[6] = w6; p[7] = w7;
@@ -412,10 +430,22 @@ DI void rec_simple(const Dev& D, X& x, uint32_t cls, uint32_t kind) {
   rec8(D, x, x.now, cls | (kind << 8) | (0xFFu << 16), x.msgs_sent, 0, 0, 0, 0, 0);
 }
 
+// A verdict stops the cluster (a Rust panic): its trace record (class 3) is the event's last.
+// Handlers return as soon as x.code leaves MR_RUNNING, before any further observable effect,
+// and nothing they do after it changes x.now or x.msgs_sent, so the record is appended once,
+// where the step loop ends the event (fail_flush) — one copy of the record path instead of one
+// inlined at each of the ~100 panic sites (MR_FAIL_DEFER; A/B in DESIGN.md §6.8)
+#ifndef MR_FAIL_DEFER
+#define MR_FAIL_DEFER 0
+#endif
 DI void fail(const Dev& D, X& x, uint32_t code) {
   if (x.code != RUN) return;
   x.code = code;
-  rec_simple(D, x, 3, code);
+  if (!MR_FAIL_DEFER) rec_simple(D, x, 3, code);
+}
+// the deferred verdict record of an event that ended the cluster (t_end records MR_PASS itself)
+DI void fail_flush(const Dev& D, X& x) {
+  if (MR_FAIL_DEFER && x.code != RUN && x.code != MR_PASS) rec_simple(D, x, 3, x.code);
 }
 
 // ---------------------------------------------------------------- timers / net
@@ -496,29 +526,41 @@ DI bool link_cut(const Dev& D, X& x, uint32_t a, uint32_t b) {
 
 // madsim net send from node `src` (whose state is `s`) (tester.rs:127-137,
 // :147-149). Returns the slot or -1 if the message is dropped.
+// `lean` (the node event's send loop, MR_SEND_LEAN): the caller has already dropped the sends
+// that clog (its `reach` mask folds in the connect state and the cut links), and records a
+// capacity verdict itself where the loop exits, so the loop body carries no clog test and no
+// inlined copy of the verdict record
+#ifndef MR_SEND_LEAN
+#define MR_SEND_LEAN 1
+#endif
 DI int net_send(const Dev& D, X& x, uint32_t src, uint32_t& nctr, uint32_t dst, uint32_t type,
                 uint32_t inc, uint32_t term, uint32_t a, uint32_t b, uint32_t c, uint64_t v,
-                uint32_t k, uint32_t ent = NONE) {
+                uint32_t k, uint32_t ent = NONE, bool lean = false) {
   // the sender in its NET draws: server src, or a clerk's 8 + clerk id (ent; SEMANTICS §12)
   const uint32_t who = ent == NONE ? src : ent;
   uint32_t seq = x.msgs_sent++;
   uint32_t ctr = nctr++;
   uint32_t w0, w1;
-  if (!bit(x.conn, src) || !bit(x.conn, dst) || link_cut(D, x, src, dst)) {
+  if (!lean && (!bit(x.conn, src) || !bit(x.conn, dst) || link_cut(D, x, src, dst))) {
     if (MR_TAPE && D.tape_mode) philox(D, x, ctr, who, ST_NET, w0, w1);  // recorded too (as the oracle)
     CADD(CNT_DROP_CLOG, 1u);
     return -1;
   }
   philox(D, x, ctr, who, ST_NET, w0, w1);
   if (w0 < net_loss(x)) { CADD(CNT_DROP_LOSS, 1u); return -1; }
-  if (x.inflight >= D.M) {  // madsim's net has no cap: a full slot table is a simulator limit
-    CADD(CNT_DROP_OVERFLOW, 1u);
-    fail(D, x, MR_FAIL_SIM_CAPACITY);
+  // madsim's net has no cap: a full slot table (SEMANTICS §9), a sequence number past 2^24
+  // (§3) or a delivery time past the key range (§4) is a simulator limit, one verdict
+  const bool full = x.inflight >= D.M;
+  if (full) CADD(CNT_DROP_OVERFLOW, 1u);
+  uint32_t t = x.now + u_range(w1, 1000u, net_lat_hi(x));
+  if (full || seq >= (1u << 24) || t >= T_KEY_MAX) {
+    if (lean) {
+      if (x.code == RUN) x.code = MR_FAIL_SIM_CAPACITY;  // recorded by the caller
+    } else {
+      fail(D, x, MR_FAIL_SIM_CAPACITY);
+    }
     return -1;
   }
-  if (seq >= (1u << 24)) { fail(D, x, MR_FAIL_SIM_CAPACITY); return -1; }  // SEMANTICS §3, §9
-  uint32_t t = x.now + u_range(w1, 1000u, net_lat_hi(x));
-  if (t >= T_KEY_MAX) { fail(D, x, MR_FAIL_SIM_CAPACITY); return -1; }  // SEMANTICS §4
   uint32_t slot = 0;
   if constexpr (MW == 1) {
     slot = (uint32_t)__builtin_ctzll(x.free_mask[0]);
@@ -569,6 +611,12 @@ DI int net_send(const Dev& D, X& x, uint32_t src, uint32_t& nctr, uint32_t dst, 
 constexpr uint32_t HDR_MAT = 1u << 28;  // message header: payload copied into D.pay
 constexpr uint32_t LAT_BOUND_US = 27000u;
 
+// a node event's pending payload range (NF_PLO, NF_PHI) loaded with its record (before round 3's
+// second half this switch was tested before its definition and so was always off: pend_note and
+// the AppendEntries write guard reloaded the range after the sends, waiting on their stores)
+#ifndef MR_PLO_EARLY
+#define MR_PLO_EARLY 1
+#endif
 DI void pend_note(const Dev& D, X& x, uint32_t me, NC& d, uint32_t lo, uint32_t hi,
                   uint32_t olo_early = 0, uint32_t ohi_early = 0) {
   uint32_t plo = lo, phi = hi;
@@ -632,9 +680,6 @@ DI void guard_log_write(const Dev& D, X& x, uint32_t L, uint32_t& pexp, uint32_t
 constexpr uint32_t AC = MR_AC;  // entries per batch of independent loads in log walks
 #ifndef MR_SEND_EARLY  // a leader's append-term loads issued before the applier (A/B in DESIGN.md §6)
 #define MR_SEND_EARLY 1
-#endif
-#ifndef MR_PLO_EARLY
-#define MR_PLO_EARLY 1
 #endif
 #ifndef MR_AP_PIPE  // software-pipelined applier batches (node_apply); A/B in DESIGN.md §6
 #define MR_AP_PIPE 1
@@ -921,6 +966,9 @@ DI void node_apply_coop(const Dev& D, X& x, uint32_t me, NC& d) {
       e = D.log[((size_t)oc * D.n + ome) * D.log_cap + (i & (D.log_cap - 1u))];
       s = D.stor[(size_t)oc * D.apply_cap + i];
     }
+    // the entry is consumed here on every path (not only where it is stored): a load left pending
+    // past the applier makes the step loop's next write to that register wait on vmcnt(0)
+    asm volatile("" ::"v"(e.term), "v"(e.val));
     uint32_t key = ~0u;
     if (mine) {
       if (!inb) key = (i << 2) | 0u;                                    // SIM_CAPACITY
@@ -1082,6 +1130,9 @@ DI void node_event(const Dev& D, X& x, bool is_msg, uint32_t tnode, uint32_t slo
   uint32_t me = tnode, src = 0, type = 0, inc = 0, k = 0, mterm = 0, ma = 0, mb = 0, mc = 0;
   bool kvready = false;
   uint32_t hdr_bits = 0;
+#ifdef MR_DEV_PRIO  // A/B: the wave issuing an event's first loads ahead of the SIMD's other wave
+  __builtin_amdgcn_s_setprio(MR_DEV_PRIO);
+#endif
 #ifndef MR_NODE_FIRST  // the node record's loads issued before the message is decoded
 #define MR_NODE_FIRST 1
 #endif
@@ -1115,6 +1166,17 @@ DI void node_event(const Dev& D, X& x, bool is_msg, uint32_t tnode, uint32_t slo
       for (uint32_t w = 0; w < MW; w++) x.free_mask[w] |= (slot >> 6) == w ? 1ull << (slot & 63u) : 0ull;
     }
     x.inflight--;
+#ifdef MR_DEV_DUP_RESCAN  // timing only: the rescan done twice
+    {
+      uint64_t fm = x.free_mask[0];
+      asm volatile("" : "+v"(fm));
+      x.free_mask[0] = fm;
+      rescan_min(D, x);
+      uint64_t mm = x.mmin;
+      asm volatile("" : "+v"(mm));
+      x.mmin = mm;
+    }
+#endif
     rescan_min(D, x);
     PROF(P_DECODE);
     if constexpr (KV) {
@@ -1136,6 +1198,39 @@ DI void node_event(const Dev& D, X& x, bool is_msg, uint32_t tnode, uint32_t slo
 #endif
 #endif
   PROF(P_LOAD);
+#ifndef MR_WAIT_HYGIENE
+// Loads whose first use the compiler would otherwise place after stores (the pending payload
+// range, read after the send loop; a snapshot value read inside it) make that use wait on
+// vmcnt(0), i.e. on every store issued since (vmcnt counts loads and stores in issue order):
+// the range is consumed here, with the node record, and the snapshot value is loaded where an
+// InstallSnapshot is sent (A/B in DESIGN.md §6.8)
+#define MR_WAIT_HYGIENE 1
+#endif
+  uint2 prange_r = prange;
+#if MR_WAIT_HYGIENE  // opaque from here on: kept in registers, never reloaded after the sends
+  asm volatile("" : "+v"(prange_r.x), "+v"(prange_r.y));
+#endif
+#ifdef MR_DEV_PRIO
+  __builtin_amdgcn_s_setprio(0);
+#endif
+#ifdef MR_DEV_EXTRA_RT  // timing only: one more dependent round trip per node event
+  {
+    uint32_t z = d.f;
+    asm volatile("" : "+v"(z));
+    z &= 0u;
+    asm volatile("" : "+v"(z));
+    const uint32_t v = NDP(me)[NF_PEXP + z];
+    asm volatile("" ::"v"(v));
+  }
+#endif
+#ifdef MR_DEV_EXTRA_VALU  // timing only: MR_DEV_EXTRA_VALU more VALU instructions per node event
+  {
+    uint32_t z = x.now;
+#pragma unroll
+    for (int i = 0; i < MR_DEV_EXTRA_VALU; i++) asm volatile("v_add_u32 %0, %0, 1" : "+v"(z));
+    asm volatile("" ::"v"(z));
+  }
+#endif
   // election-timer resets (raft.rs:260-263) are counted where the handlers call them and
   // drawn once, after the handler: the timer keeps only the last draw, each draw is keyed by
   // its own ectr (SEMANTICS §2), and nothing between reads the timer, so one Philox site
@@ -1290,7 +1385,11 @@ DI void node_event(const Dev& D, X& x, bool is_msg, uint32_t tnode, uint32_t slo
               continue;
             }
             if (i - d.snap > D.log_cap) { fail(D, x, MR_FAIL_SIM_CAPACITY); return; }
+#if MR_PLO_EARLY
+            guard_log_write(D, x, me, d.pexp, i, prange_r.x, prange_r.y);
+#else
             guard_log_write(D, x, me, d.pexp, i);
+#endif
             rsprev = pe[q].term == tprev ? rsprev : i;
             tprev = pe[q].term;
             D.log[logi(D, x, me, i)] = LE{pe[q].term, rsprev, pe[q].val};
@@ -1381,7 +1480,10 @@ DI void node_event(const Dev& D, X& x, bool is_msg, uint32_t tnode, uint32_t slo
 #ifndef MR_CLOG_FAST
 #define MR_CLOG_FAST 1
 #endif
-  const uint32_t reach = (MR_TAPE || !MR_CLOG_FAST) ? ~0u : (bit(x.conn, me) ? x.conn : 0u);
+  uint32_t reach = (MR_TAPE || !MR_CLOG_FAST) ? ~0u : (bit(x.conn, me) ? x.conn : 0u);
+  constexpr bool lean = MR_SEND_LEAN && !MR_TAPE && MR_CLOG_FAST;
+  if (lean && D.links)  // links cut by disconnect2 / partition (link_cut): word me / 4, byte me % 4
+    reach &= ~((CS(CS_CUT + (me >> 2)) >> (8u * (me & 3u))) & 0xFFu);
 #if MR_SEND_EARLY
   // a leader's appends read our terms at next[p] - 1: issue those loads before the applier's
   // checker stores (the ring slot is valid whatever the applier does; gated after it)
@@ -1432,23 +1534,37 @@ DI void node_event(const Dev& D, X& x, bool is_msg, uint32_t tnode, uint32_t slo
       LNX(p) = nxa[p];
       LPT(p) = pv == 0u ? 0u : pv == d.snap ? d.snapt : pv == d.last ? d.lastt : pv > lbase ? d.term : t;
     }
-    if (any_is) snapv = NSV(me);
+    if (!MR_WAIT_HYGIENE && any_is) snapv = NSV(me);
   }
   uint32_t plo_acc = ~0u, phi_acc = 0u;  // index range referenced by this event's payloads
+#ifndef MR_SEND_HOIST  // the fields every send of the event shares, chosen once before the loop
+#define MR_SEND_HOIST 1
+#endif
+  // a reply or a vote request carries the same fields to every peer; an append's come from
+  // the peer's next[] (LDS staging) inside the loop
+  const bool rep = mode == SEND_REPLY;
+  const uint32_t st0 = rep ? rtype : M_RV_REQ, sa0 = rep ? ra : me, sb0 = rep ? rb : d.last,
+                 sc0 = rep ? 0u : lt, sinc = rep ? inc : f_inc(d.f);
+  bool sfail = false;  // a send hit a simulator limit (lean sends: recorded after the loop)
+  uint32_t sclog = 0;  // ... and the clogged sends before it
   while (peers) {  // the single send path: ascending peer order over the reachable peers
     uint32_t p = (uint32_t)__builtin_ctz(peers);
     peers &= peers - 1u;
     const uint32_t below = all & ((1u << p) - 1u);  // earlier sends of this event, clogged ones too
     x.msgs_sent = seq0 + (uint32_t)__builtin_popcount(below);
     d.nctr = ctr0 + (uint32_t)__builtin_popcount(below);
-    uint32_t st = M_RV_REQ, sa = me, sb = d.last, sc = lt, sk = 0, sinc = f_inc(d.f), prev = 0;
+    uint32_t st, sa, sb, sc, sk = 0, prev = 0;
     uint64_t sv = 0;
-    if (mode == SEND_REPLY) {
-      st = rtype; sa = ra; sb = rb; sc = 0; sinc = inc;
-    } else if (mode == SEND_APPEND) {
+    if (MR_SEND_HOIST) {
+      st = st0; sa = sa0; sb = sb0; sc = sc0;
+    } else {
+      st = M_RV_REQ; sa = me; sb = d.last; sc = lt;
+      if (mode == SEND_REPLY) { st = rtype; sa = ra; sb = rb; sc = 0; }
+    }
+    if (mode == SEND_APPEND) {
       const uint32_t nx = LNX(p);
-      if (nx <= d.snap) {
-        st = M_IS_REQ; sa = d.snap; sb = d.snapt; sc = 0; sv = snapv;
+      if (has_snaps(S) && nx <= d.snap) {
+        st = M_IS_REQ; sa = d.snap; sb = d.snapt; sc = 0; sv = MR_WAIT_HYGIENE ? NSV(me) : snapv;
       } else {
         prev = nx - 1;
         sk = d.last - prev;
@@ -1457,10 +1573,11 @@ DI void node_event(const Dev& D, X& x, bool is_msg, uint32_t tnode, uint32_t slo
       }
     }
     PROF(P_S_SETUP);
-    int s = net_send(D, x, me, d.nctr, p, st, sinc, d.term, sa, sb, sc, sv, sk);
+    int s = net_send(D, x, me, d.nctr, p, st, sinc, d.term, sa, sb, sc, sv, sk, NONE, lean);
     if (x.code != RUN) {  // the clogged sends before this one are counted as they happened
-      CADD(CNT_DROP_CLOG, (uint32_t)__builtin_popcount(below & ~reach));
-      return;
+      sfail = true;
+      sclog = (uint32_t)__builtin_popcount(below & ~reach);
+      break;
     }
     PROF(P_S_NET);
     if (s >= 0 && sk) {  // zero-copy payload: entries prev+1 .. prev+sk stay in this log
@@ -1469,10 +1586,15 @@ DI void node_event(const Dev& D, X& x, bool is_msg, uint32_t tnode, uint32_t slo
       PROF(P_S_PAY);
     }
   }
+  if (sfail) {
+    if (lean && !MR_FAIL_DEFER) rec_simple(D, x, 3, x.code);  // the verdict net_send left unrecorded
+    CADD(CNT_DROP_CLOG, sclog);
+    return;
+  }
   x.msgs_sent = seq0 + (uint32_t)__builtin_popcount(all);  // every send of the event, clogged too
   d.nctr = ctr0 + (uint32_t)__builtin_popcount(all);
   CADD(CNT_DROP_CLOG, (uint32_t)__builtin_popcount(all & ~reach));
-  if (plo_acc <= phi_acc) pend_note(D, x, me, d, plo_acc, phi_acc, prange.x, prange.y);
+  if (plo_acc <= phi_acc) pend_note(D, x, me, d, plo_acc, phi_acc, prange_r.x, prange_r.y);
   if constexpr (KV) {
     if (kvready) {
       kv_flush(D, x, me, d);
@@ -1655,6 +1777,9 @@ DI uint32_t nd_term(const Dev& D, X& x, uint32_t i) { return ND(NF_TERM, i); }
 template <uint32_t S>
 DI void tester(const Dev& D, X& x) {
   T t;
+#ifdef MR_DEV_PRIO
+  __builtin_amdgcn_s_setprio(MR_DEV_PRIO);
+#endif
   uint32_t pcw = CS(CS_TPC);
   t.pc = pcw & 0xFFFFFFu;
   t.helper = pcw >> 24;
@@ -1664,6 +1789,9 @@ DI void tester(const Dev& D, X& x) {
 #pragma unroll
   for (uint32_t k = 0; k < T_NH; k++) t.h[k] = CS(CS_TH + k);
   t.hv = C64(C64_THV);
+#ifdef MR_DEV_PRIO
+  __builtin_amdgcn_s_setprio(0);
+#endif
   x.yield = 0;
   for (int guard = 0;; guard++) {
     if (guard > 4096) { fail(D, x, MR_FAIL_SIM_BAD_PROGRAM); return; }
@@ -1731,6 +1859,23 @@ DI void lane_load(const Dev& D, X& x) {
   for (uint32_t k = 0; k < CNT__N; k++) x.cnt[k] = CS(CS_CNT + k);
 #endif
   for (uint32_t s = 0; s < D.M; s++) LK(s) = (lkey_t)MKEY(s);
+  // every load above completes here (each loaded register is read by an empty asm): a lane that
+  // takes a new cluster inside the step loop (streaming) then leaves no load pending into the
+  // loop, where the compiler would otherwise place a conservative vmcnt(0) — one that also
+  // waits for every store in flight — at the first later use of these registers on EVERY
+  // iteration's path
+  asm volatile("" ::"v"(x.now), "v"(x.events), "v"(x.msgs_sent), "v"(x.inflight), "v"(x.trace_n),
+               "v"(x.mslot), "v"(x.netmode), "v"(x.t_ctr), "v"(x.conn), "v"(x.alive), "v"(x.twake),
+               "v"(x.lmask), "v"(x.digest), "v"(x.mmin));
+  if constexpr (nthr(S) > 0) asm volatile("" ::"v"(x.cwake), "v"(x.ctid), "v"(x.cslot));
+#pragma unroll
+  for (uint32_t d = 0; d < NB; d++) asm volatile("" ::"v"(x.timer[d]));
+#pragma unroll
+  for (uint32_t w = 0; w < MW; w++) asm volatile("" ::"v"(x.free_mask[w]));
+#if !MR_CNT_MEM
+#pragma unroll
+  for (uint32_t k = 0; k < CNT__N; k++) asm volatile("" ::"v"(x.cnt[k]));
+#endif
 }
 template <uint32_t S>
 DI void lane_store(const Dev& D, X& x) {
@@ -1783,7 +1928,10 @@ DI bool lane_claim(const Dev& D, X& x, bool want) {
 // message slots (LDS for one wave per SIMD), so they take the whole register file and keep
 // their overflow in AGPRs instead of scratch (config 5: 299 -> 265 ms)
 template <uint32_t S>
-constexpr uint32_t step_waves() { return is_svc(S) ? 1u : (uint32_t)MR_WAVES_PER_EU; }
+#ifndef MR_SVC_WAVES
+#define MR_SVC_WAVES 1
+#endif
+constexpr uint32_t step_waves() { return is_svc(S) ? (uint32_t)MR_SVC_WAVES : (uint32_t)MR_WAVES_PER_EU; }
 template <uint32_t S, uint32_t NBT>
 __global__ void __launch_bounds__(STEP_BLOCK, step_waves<S>()) step_kernel(Dev D, uint32_t budget) {
   static_assert(NBT == NB, "one node bound per translation unit");
@@ -1885,12 +2033,13 @@ __global__ void __launch_bounds__(STEP_BLOCK, step_waves<S>()) step_kernel(Dev D
     if (!run || !mine) continue;
     if (nthr(S) > 0 && (uint32_t)(key >> 32) == INF_T) {  // nothing can wake the test body
       fail(D, x, MR_FAIL_SIM_BAD_PROGRAM);
+      fail_flush(D, x);
       continue;
     }
     x.now = (uint32_t)(key >> 32);
     need = true;
     x.events++;
-    if (x.events > D.max_events) { fail(D, x, MR_FAIL_SIM_EVENT_LIMIT); continue; }
+    if (x.events > D.max_events) { fail(D, x, MR_FAIL_SIM_EVENT_LIMIT); fail_flush(D, x); continue; }
     if (cls != CLS_TESTER) {
       CADD(cls == CLS_MSG ? CNT_EV_MSG : CNT_EV_TIMER, 1u);
       NR nr;
@@ -1908,6 +2057,7 @@ __global__ void __launch_bounds__(STEP_BLOCK, step_waves<S>()) step_kernel(Dev D
       }
       PROF(P_TESTER);
     }
+    fail_flush(D, x);
   }
 #ifdef MR_PROF
   PROF(P_TAIL);

@@ -24,6 +24,8 @@ tag = sys.argv[1]
 names = sys.argv[2].split(",") if len(sys.argv) > 2 else list(CONFIGS)
 for name in names:
     test, c, kw = CONFIGS[name]
+    if os.environ.get("LPW"):  # lanes per wave (0 = auto)
+        kw = dict(kw, lanes_per_wave=int(os.environ["LPW"]))
     with sim.Batch(test, c, **kw) as b:
         b.run()
         ms = ev = 0.0
