@@ -1731,8 +1731,35 @@ DI uint32_t t_term(const Dev& D, X& x, uint32_t i) {
   if (!bit(x.alive, i)) { fail(D, x, MR_FAIL_UNWRAP_NONE); return 0; }
   return ND(NF_TERM, i);
 }
+// The tester's checks over every server read each record's words as one batch of loads
+// (unrolled over the node bound): a loop that loads server by server is one round trip per
+// server, and one per server index some lane needs (MR_T_BATCH; A/B in DESIGN.md ยง6.8)
+#ifndef MR_T_BATCH  // (the 8-server instances keep the loops: see MR_T_ONEWALK, mr_tester.inc)
+#define MR_T_BATCH (MR_NB <= 7)
+#endif
+// the terms of every server (words NF_TERM), 0 past D.n
+DI void t_terms(const Dev& D, X& x, uint32_t (&tm)[NB]) {
+#pragma unroll
+  for (uint32_t q = 0; q < NB; q++) tm[q] = q < D.n ? ND(NF_TERM, q) : 0u;
+}
 DI uint32_t t_log_size(const Dev& D, X& x) {  // tester.rs:152-158 + SEMANTICS ยง5 size model
   uint32_t mx = 0;
+  if (MR_T_BATCH) {
+    uint32_t fl[NB], la[NB], sn[NB];
+#pragma unroll
+    for (uint32_t q = 0; q < NB; q++) {
+      const bool in = q < D.n;
+      fl[q] = in ? ND(NF_FLAGS, q) : 0u;
+      la[q] = in ? ND(NF_LAST, q) : 0u;
+      sn[q] = in ? ND(NF_SNAP, q) : 0u;
+    }
+#pragma unroll
+    for (uint32_t q = 0; q < NB; q++) {
+      const uint32_t sz = 32u + (f_voted(fl[q]) != 15u ? 9u : 1u) + 24u * (la[q] - sn[q]);
+      if (q < D.n && sz > mx) mx = sz;
+    }
+    return mx;
+  }
   for (uint32_t i = 0; i < D.n; i++) {
     uint32_t sz = 32u + (f_voted(ND(NF_FLAGS, i)) != 15u ? 9u : 1u) +
                   24u * (ND(NF_LAST, i) - ND(NF_SNAP, i));
@@ -1742,10 +1769,12 @@ DI uint32_t t_log_size(const Dev& D, X& x) {  // tester.rs:152-158 + SEMANTICS ย
 }
 DI uint32_t t_check_terms(const Dev& D, X& x) {  // tester.rs:95-109
   uint32_t term = 0;
+  uint32_t tm[NB];
+  if (MR_T_BATCH) t_terms(D, x, tm);
   for (uint32_t i = 0; i < D.n; i++) {
     if (!bit(x.conn, i)) continue;
     if (!bit(x.alive, i)) { fail(D, x, MR_FAIL_UNWRAP_NONE); return 0; }
-    uint32_t xt = ND(NF_TERM, i);
+    uint32_t xt = MR_T_BATCH ? sel_nb(tm, i) : ND(NF_TERM, i);
     if (term == 0) term = xt;
     else if (term != xt) { fail(D, x, MR_FAIL_TERM_DISAGREE); return 0; }
   }
