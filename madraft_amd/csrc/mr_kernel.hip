@@ -1103,9 +1103,10 @@ DI void ae_load_batch(const Dev& D, const X& x, uint32_t me, const NC& d, uint32
     const uint32_t jx = j + q, i = ma + 1 + jx;
     pe[q] = jx < k ? (mat ? pp[jx] : D.log[logi(D, x, src, i)]) : LE{};
 #if MR_AE_OWN
-    // i > snap here (the caller skips a payload's prefix at or below the snapshot); the ring
-    // slot of any i is a valid address, so the safety checks' loads need no bound
-    const bool own = jx < k && (i <= d.last || D.safety);
+    // i > snap here (the caller skips a payload's prefix at or below the snapshot). Only
+    // entries we hold are loaded: the log-matching check reads a command only where i <= last
+    // (loading every slot under MR_F_SAFETY measured -2.0 %, profiles/r03b_ab.txt e17)
+    const bool own = jx < k && i <= d.last;
     const LE o = own ? D.log[logi(D, x, me, i)] : LE{};
     lt[q] = (jx < k && i <= d.last) ? (i == d.last ? d.lastt : o.term) : 0u;
     ov[q] = o.val;
