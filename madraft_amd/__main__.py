@@ -9,6 +9,14 @@ import time
 from . import _abi, sim, trace
 
 
+def net_mode(test, unreliable_flag):
+    """The network mode a replayed log's sends were drawn under when a line does not say:
+    `--unreliable` (MR_F_UNRELIABLE from the tester's start), else the test body's own mode —
+    the tests named *unreliable* switch the net to unreliable (tester.rs:127-137), the others
+    run it reliable. A line's own "unreliable" field still wins (trace.decisions_from_events)."""
+    return bool(unreliable_flag) or "unreliable" in test
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("test")
@@ -29,7 +37,8 @@ def main():
         flags |= {"vote_twice": _abi.MR_F_BUG_VOTE_TWICE, "vote_stale": _abi.MR_F_BUG_VOTE_STALE,
                   "no_prev_check": _abi.MR_F_BUG_NO_PREV_CHECK}[a.bug]
     if a.replay:
-        tr, code, tm, misses = sim.replay(a.test, trace.load_jsonl(a.replay, unreliable=True if a.unreliable else None), seed=a.seed or _abi.README_SEED,
+        dec = trace.load_jsonl(a.replay, unreliable=net_mode(a.test, a.unreliable))
+        tr, code, tm, misses = sim.replay(a.test, dec, seed=a.seed or _abi.README_SEED,
                                           nodes=a.nodes, iters=a.iters, unreliable=a.unreliable,
                                           null_raft=a.null, safety=a.safety, flags=flags)
         print(json.dumps({"code": code, "verdict": _abi.FAIL_NAMES.get(code, str(code)),

@@ -635,8 +635,6 @@ uint32_t mr_decision_word(uint32_t v, uint32_t lo, uint32_t hi) {
 static void drop_decisions(mr_batch* b) {
   if (b->tape) (void)hipFree(b->tape);
   if (b->doff) (void)hipFree(b->doff);
-  if (b->held[0]) (void)hipFree(b->held[0]);
-  if (b->held[1]) (void)hipFree(b->held[1]);
   b->tape = nullptr;
   b->doff = nullptr;
   b->D.dtab = nullptr; b->D.doff = nullptr; b->D.dcap = 0; b->D.tape_mode = 0;
@@ -777,6 +775,9 @@ void mr_batch_destroy(mr_batch* b) {
   if (b->base) (void)hipFree(b->base);
   if (b->tape) (void)hipFree(b->tape);
   if (b->doff) (void)hipFree(b->doff);
+  // the streaming held-cluster lists belong to the batch, not to its decision tables
+  for (uint32_t h = 0; h < 2; h++)
+    if (b->held[h]) { (void)hipFree(b->held[h]); b->held[h] = nullptr; }
   if (b->red) (void)hipFree(b->red);
   if (b->h_remaining) (void)hipHostFree(b->h_remaining);
   if (b->h_ctl0) (void)hipHostFree(b->h_ctl0);

@@ -91,6 +91,9 @@ struct X {
 #define MR_BLOCK 64  // A/B round 2 (with AC 4): configs 2-4 +2.4-10 %, config 5 -1 % (r02_s2r)
 #endif
 constexpr uint32_t STEP_BLOCK = MW > 2 ? 64 : MR_BLOCK;
+// the step kernel maps lane l < lpw of block b to cluster b * lpw + l (lanes_per_wave): one
+// 64-lane wave per block, which the capacity math (cap * lpw / 64) assumes too
+static_assert(STEP_BLOCK == 64, "step_kernel's lane mapping assumes one 64-lane wave per block");
 // MR_KEY32: a 32-bit LDS key t << 5 | dst (t < 2^27 - 1, SEMANTICS §4); the (rare) tie of
 // two messages at the same t is broken by their sequence numbers, kept in the message
 // record (word MF_PAD). Otherwise a 64-bit key (t << 32 | seq << 6 | ae << 5 | dst).

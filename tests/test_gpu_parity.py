@@ -162,6 +162,25 @@ def test_lanes_chunks_and_streaming(hip, oracle, lanes, stream):
         assert np.array_equal(a_, c_)
 
 
+def test_streaming_after_set_decisions(hip):
+    """A streaming batch whose decision table is set and dropped keeps its held-cluster lists
+    (they were freed with the decision table, then written by the next launch)."""
+    with hip.Batch("figure_8_unreliable_2c", 700, iters=100) as b:
+        b.run()
+        ref = b.verdicts()
+    with hip.Batch("figure_8_unreliable_2c", 700, iters=100, lanes=128, stream=True) as b:
+        b.set_decisions(None)
+        for _ in range(2):  # a launch, then another set + drop between launches of one run
+            b.run(max_events=2001)
+            b.set_decisions(None)
+        while b.run(max_events=2001)["remaining"]:
+            pass
+        got = b.verdicts()
+        assert b.counters()["done"] == 700
+    for a_, c_ in zip(ref, got):
+        assert np.array_equal(a_, c_)
+
+
 @pytest.mark.parametrize("lpw", [64, 32, 16])
 @pytest.mark.parametrize("test,kw", [("figure_8_unreliable_2c", dict(iters=200)),
                                      ("fail_agree_2b", dict(nodes=5, unreliable=True)),

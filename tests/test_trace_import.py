@@ -108,6 +108,18 @@ def test_send_mode_and_dropped_defaults():
     assert int(dropped["w0"][0]) < _abi.LOSS_Q32
 
 
+def test_cli_net_mode_defaults_to_the_tests_own():
+    """A replayed log whose send lines carry no mode takes the run's: --unreliable, else the
+    test body's (reliable for initial_election_2a, unreliable for figure_8_unreliable_2c)."""
+    from madraft_amd.__main__ import net_mode
+    assert net_mode("initial_election_2a", False) is False
+    assert net_mode("initial_election_2a", True) is True
+    assert net_mode("figure_8_unreliable_2c", False) is True
+    line = {"event": "send", "host": 0, "index": 0, "latency_us": 9000}
+    rel = trace.decisions_from_events([line], unreliable=net_mode("basic_agree_2b", False))
+    assert trace.events_from_decisions(rel, unreliable=False)[0]["latency_us"] == 9000
+
+
 @pytest.mark.gpu
 def test_gpu_replays_an_imported_event_log(hip, oracle, tmp_path):
     cfg = oracle.cfg("figure_8_unreliable_2c", iters=100)
@@ -141,3 +153,22 @@ def test_cli_replays_a_hand_written_log(hip, tmp_path):
     assert r.returncode == 0, r.stderr
     out = json.loads(r.stdout.strip().splitlines()[-1])
     assert out["code"] == 0 and out["events"] > 0 and out["misses"] > 0
+
+
+@pytest.mark.gpu
+def test_cli_replays_a_reliable_log_without_modes(hip, tmp_path):
+    """The same hand-written run with no per-line "unreliable": the reliable test's own mode
+    decodes the sends (the CLI used to reject such a log)."""
+    import subprocess
+    import sys
+    lines = [json.dumps({"event": "election_timeout", "node": i, "index": 0,
+                         "timeout_us": 150000 if i == 0 else 299000}) for i in range(3)]
+    lines += [json.dumps({"event": "send", "host": h, "index": k, "latency_us": 1000})
+              for h in range(3) for k in range(4)]
+    p = tmp_path / "hand_rel.jsonl"
+    p.write_text("\n".join(lines) + "\n")
+    r = subprocess.run([sys.executable, "-m", "madraft_amd", "initial_election_2a", "--replay", str(p)],
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    out = json.loads(r.stdout.strip().splitlines()[-1])
+    assert out["code"] == 0 and out["events"] > 0
