@@ -246,6 +246,13 @@ def main():
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
                      "traffic": traffic,
                      "traffic_over_alg": round(traffic / per_launch, 3) if traffic else None,
+                     # wavefront divergence and LDS bank conflicts of the same build (rocprofv3
+                     # --pmc: SQ_THREAD_CYCLES_VALU / SQ_ACTIVE_INST_VALU / 64, calibrated by
+                     # tools/valu_calib.hip; SQ_LDS_BANK_CONFLICT per launch), or null
+                     "valu_lane_util": round(pmc["valu_lane_util"], 4) if pmc and "valu_lane_util" in pmc else None,
+                     "lds_bank_conflicts": pmc.get("lds_bank_conflicts_per_launch") if pmc else None,
+                     "valu_insts_per_event": (round(pmc["sq_insts_valu_per_launch"] / (r0["events"] / max(r0["launches"], 1)), 2)
+                                              if pmc and "sq_insts_valu_per_launch" in pmc else None),
                      "traffic_source": (f"{pmc['file']} (lib {lib_sha}): {pmc.get('method', '')}"
                                         if pmc else f"no PMC record of lib {lib_sha} on this workload"),
                      "kernel": "step_kernel",

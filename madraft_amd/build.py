@@ -38,12 +38,16 @@ NB7_SCNS = {19, 20, 21, 22, 23}
 DEFAULT_N = [0, 3, 3, 7, 5, 3, 5, 3, 3, 5, 3, 3, 5, 3, 5, 5, 5, 5, 5, 3, 3, 3, 3, 3, 5, 5, 5, 5, 3, 3, 5, 5, 5, 5, 5, 5, 5, 3, 5, 3, 3, 5, 5, 5, 5, 5, 7, 7]
 
 
+def has_exact(i, nb):
+    """mr_dev.h has_exact: an exact-size instance (NB = n < 8) of scenario i is built."""
+    return nb < 8 and (DEFAULT_N[i] == nb or (i == 5 and nb == 5) or (i in NB7_SCNS and nb == 7))
+
+
 def _units(csrc, scns=None):
     kern = os.path.join(csrc, "mr_kernel.hip")
     units = [(kern, "common", ["-DMR_COMMON=1", "-DMR_SCN_LIST=", "-DMR_NB=8"])]
     for nb in (3, 5, 7, 8):
-        ids = [i for i in (scns or SCN_IDS)
-               if nb == 8 or (DEFAULT_N[i] == nb if nb != 7 else i in NB7_SCNS)]
+        ids = [i for i in (scns or SCN_IDS) if nb == 8 or has_exact(i, nb)]
         if not ids:
             continue
         wide = [i for i in ids if i in WIDE_SLOTS]

@@ -279,6 +279,15 @@ constexpr uint32_t nb_of(uint32_t s) { return k_default_n[s] <= 5 ? k_default_n[
 constexpr bool has_nb7(uint32_t s) {
   return s >= MR_SCN_SNAPSHOT_BASIC_2D && s <= MR_SCN_SNAPSHOT_INSTALL_UNRELIABLE_CRASH_2D;
 }
+// exact-size step-kernel instances (NB = n < 8): the node count is a compile-time constant there
+// (every `q < n` over the unrolled node loops folds away, and with it the loop-invariant lane
+// masks the compiler otherwise keeps in scalar registers); any other n runs the generic 8-server
+// instance. Built: each scenario at its default n, BASELINE config 2 (fail_agree_2b at 5
+// servers) and config 4 (the 2D tests at 7)
+constexpr bool has_exact(uint32_t s, uint32_t n) {
+  return n < 8u && (n == k_default_n[s] || (s == MR_SCN_FAIL_AGREE_2B && n == 5u) ||
+                    (has_nb7(s) && n == 7u));
+}
 // scenarios whose test body starts the tester with service snapshots (t_new(snapshot = true),
 // tester.rs:303-325 SNAPSHOT_INTERVAL): snap_common's five 2D tests. node_apply_coop specializes
 // on it at compile time and checks it against the runtime mode (x.netmode bit 1).

@@ -16,17 +16,28 @@
 #include "mr_dev.h"
 
 namespace mr {
-// the 7-server instance of S, where one is built (else the 8-server one: never reached)
-#define NB7_OF(S) (has_nb7(S) ? 7u : (uint32_t)MR_MAX_NODES)
+// the step-kernel instance of scenario S for D.n servers: the exact-size one where it is built
+// (mr_dev.h has_exact), else the generic 8-server one
+template <uint32_t S>
+static hipError_t launch_any(const Dev& D, uint32_t budget, hipStream_t s) {
+  if (D.tape_mode) return launch_step_tape_t<S, MR_MAX_NODES>(D, budget, s);
+  if constexpr (has_exact(S, 3)) if (D.n == 3) return launch_step_t<S, 3>(D, budget, s);
+  if constexpr (has_exact(S, 5)) if (D.n == 5) return launch_step_t<S, 5>(D, budget, s);
+  if constexpr (has_exact(S, 7)) if (D.n == 7) return launch_step_t<S, 7>(D, budget, s);
+  return launch_step_t<S, MR_MAX_NODES>(D, budget, s);
+}
+template <uint32_t S>
+static uint32_t capacity_any(const Dev& D, int device) {
+  if constexpr (has_exact(S, 3)) if (D.n == 3) return step_capacity_t<S, 3>(device, D.M);
+  if constexpr (has_exact(S, 5)) if (D.n == 5) return step_capacity_t<S, 5>(device, D.M);
+  if constexpr (has_exact(S, 7)) if (D.n == 7) return step_capacity_t<S, 7>(device, D.M);
+  return step_capacity_t<S, MR_MAX_NODES>(device, D.M);
+}
 // the step-kernel instance of scenario `scn` (instances: MR_ALL_SCNS)
 hipError_t launch_step(const Dev& D, uint32_t scn, uint32_t budget, hipStream_t s) {
   switch (scn) {
-#define MR_INST(S)                                                                  \
-  case S:                                                                           \
-    return D.tape_mode ? launch_step_tape_t<S, MR_MAX_NODES>(D, budget, s)          \
-           : D.n <= nb_of(S)            ? launch_step_t<S, nb_of(S)>(D, budget, s)    \
-           : (has_nb7(S) && D.n == 7) ? launch_step_t<S, NB7_OF(S)>(D, budget, s)   \
-                                      : launch_step_t<S, MR_MAX_NODES>(D, budget, s);
+#define MR_INST(S) \
+  case S: return launch_any<S>(D, budget, s);
 #ifdef MR_DEV_SCNS  // dev variants built for a few scenarios (build.py scns=)
     MR_DEV_SCNS
 #else
@@ -39,11 +50,8 @@ hipError_t launch_step(const Dev& D, uint32_t scn, uint32_t budget, hipStream_t 
 // clusters the scenario's step kernel keeps resident (0: unknown)
 static uint32_t step_capacity(const Dev& D, uint32_t scn, int device) {
   switch (scn) {
-#define MR_INST(S)                                                       \
-  case S:                                                                \
-    return D.n <= nb_of(S)            ? step_capacity_t<S, nb_of(S)>(device, D.M)   \
-           : (has_nb7(S) && D.n == 7) ? step_capacity_t<S, NB7_OF(S)>(device, D.M)   \
-                                      : step_capacity_t<S, MR_MAX_NODES>(device, D.M);
+#define MR_INST(S) \
+  case S: return capacity_any<S>(D, device);
 #ifdef MR_DEV_SCNS
     MR_DEV_SCNS
 #else

@@ -1964,10 +1964,21 @@ template <uint32_t S>
 #ifndef MR_SVC_WAVES
 #define MR_SVC_WAVES 1
 #endif
-constexpr uint32_t step_waves() { return is_svc(S) ? (uint32_t)MR_SVC_WAVES : (uint32_t)MR_WAVES_PER_EU; }
+#ifndef MR_NB8_WAVES  // the generic 8-server instances (any node count without an exact one)
+#define MR_NB8_WAVES 1
+#endif
+constexpr uint32_t step_waves() {
+  return NB >= 8 ? (uint32_t)MR_NB8_WAVES : is_svc(S) ? (uint32_t)MR_SVC_WAVES : (uint32_t)MR_WAVES_PER_EU;
+}
+// exact-size instances (NB < 8, mr_dev.h has_exact): the node count is NB at compile time
+#ifndef MR_EXACT_N
+#define MR_EXACT_N (MR_NB < MR_MAX_NODES)
+#endif
 template <uint32_t S, uint32_t NBT>
-__global__ void __launch_bounds__(STEP_BLOCK, step_waves<S>()) step_kernel(Dev D, uint32_t budget) {
+__global__ void __launch_bounds__(STEP_BLOCK, step_waves<S>()) step_kernel(Dev Din, uint32_t budget) {
   static_assert(NBT == NB, "one node bound per translation unit");
+  Dev D = Din;
+  if constexpr (MR_EXACT_N) D.n = NB;  // the host launches this instance for D.n == NB only
   X x;
   // lanes 0 .. lpw - 1 of each 64-lane block hold clusters (D.lpw < 64: a batch smaller than the
   // resident lanes still spreads over two waves per SIMD; the other lanes idle)

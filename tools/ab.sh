@@ -1,11 +1,20 @@
 #!/bin/bash
-# dev A/B on the GPU box: tools/occ.py over variant libraries (madraft_amd/lib/var/<name>.so)
-# usage: AB="a.so b.so" SIZES=131072 M=32 bash tools/ab.sh
-cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out
+# same-box A/B of variant libraries (madraft_amd/lib/var/<name>.so, tools/var.py): a parity
+# smoke per variant (GPU vs oracle, $PTEST), then $ROUNDS alternating rounds of bench.py on each
+# test in $TESTS. usage: bash tools/ab.sh <outdir> <name1> <name2> ...
+cd "$GRAFT_REPO_ROOT"; O=gpurun_out/$1; shift; mkdir -p $O
 V=$PWD/madraft_amd/lib/var
-for r in 1 2; do
-  for f in ${AB}; do
-    MADRAFT_HIP_LIB=$V/$f timeout -k 10 240 python tools/occ.py $f ${M:-32} ${SIZES:-131072} ${TEST:-figure_8_unreliable_2c} >> gpurun_out/ab.txt 2>> gpurun_out/ab.err || { echo "FAIL $f" >> gpurun_out/ab.txt; exit 1; }
+TESTS=${TESTS:-figure_8_unreliable_2c}
+PTEST=${PTEST:-"test_scenario_bit_exact and (figure_8_unreliable_2c or figure_8_unreliable_crash)"}
+for f in "$@"; do
+  MADRAFT_HIP_LIB=$V/$f.so timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 120 --timeout-method thread -k "$PTEST" > $O/parity_$f.log 2>&1 || { echo "PARITY FAIL $f"; tail -15 $O/parity_$f.log; exit 1; }
+  echo "$f parity: $(tail -1 $O/parity_$f.log)"
+done
+for r in $(seq 1 ${ROUNDS:-2}); do
+  for t in $TESTS; do
+    for f in "$@"; do
+      MADRAFT_HIP_LIB=$V/$f.so timeout -k 10 300 python bench.py --test $t --steps ${STEPS:-3} --warmup 1 --no-cpu-baseline --variant '' $BARGS > $O/b_${t}_$f.json 2> $O/b_${t}_$f.err || { echo "BENCH FAIL $f $t"; tail -5 $O/b_${t}_$f.err; exit 1; }
+      python -c "import json; d=json.loads(open('$O/b_${t}_$f.json').read().strip().splitlines()[-1]); print('$r $t $f', d['value'], 'ms/launch %.2f' % d['roofline']['avg_launch_ms'], 'ev/seed', d['events_per_seed'])" | tee -a $O/summary.txt
+    done
   done
 done
-cat gpurun_out/ab.txt

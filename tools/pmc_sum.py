@@ -81,6 +81,24 @@ if all(k in agg for k in req):
 elif "fetch2_write_bytes_per_launch" in out:
     out.update(hbm_bytes_per_launch=out["fetch2_write_bytes_per_launch"],
                method="rocprofv3 --pmc FETCH_SIZE x 2 + WRITE_SIZE (profiles/r03_fetch_calibration.txt)")
+# divergence and LDS (north_star: "LDS bank-conflict and wavefront-divergence counters"):
+# SQ_THREAD_CYCLES_VALU / SQ_ACTIVE_INST_VALU is the mean number of active lanes per VALU
+# instruction — calibrated on this pool with tools/valu_calib.hip (64 / 32 / 16 / 4 / 1 active
+# lanes read 64.0 / 32.0 / 16.1 / 4.1 / 1.08, profiles/r04_valu_calib.txt) — so / 64 is the
+# thread-level VALU utilisation; SQ_LDS_BANK_CONFLICT counts the extra LDS cycles bank conflicts
+# cost, over SQ_LDS_IDX_ACTIVE (all LDS-array cycles)
+if "SQ_THREAD_CYCLES_VALU" in agg and "SQ_ACTIVE_INST_VALU" in agg:
+    out["valu_lane_util"] = agg["SQ_THREAD_CYCLES_VALU"] / agg["SQ_ACTIVE_INST_VALU"] / 64.0
+    print(f"valu_lane_util = {out['valu_lane_util']:.4f} "
+          f"({agg['SQ_THREAD_CYCLES_VALU'] / agg['SQ_ACTIVE_INST_VALU']:.2f} active lanes per VALU instruction)")
+if "SQ_LDS_BANK_CONFLICT" in agg:
+    out["lds_bank_conflicts_per_launch"] = per_launch("SQ_LDS_BANK_CONFLICT")
+    if agg.get("SQ_LDS_IDX_ACTIVE"):
+        out["lds_bank_conflict_frac"] = agg["SQ_LDS_BANK_CONFLICT"] / agg["SQ_LDS_IDX_ACTIVE"]
+    print(f"lds_bank_conflicts per launch = {out['lds_bank_conflicts_per_launch']:.4g}")
+for k in ("SQ_INSTS_VALU", "SQ_INSTS_SALU"):
+    if k in agg:
+        out[k.lower() + "_per_launch"] = per_launch(k)
 if a.json:
     if lib is None:
         raise SystemExit("no lib_sha16 in the bench logs: cannot stamp the record")
