@@ -166,6 +166,10 @@ def main():
     ap.add_argument("--variant", default="figure_8_unreliable_crash",
                     help="second workload timed on the same shard ('' = none)")
     ap.add_argument("--variant-steps", type=int, default=2)
+    ap.add_argument("--million", type=int, default=1 << 20,
+                    help="N = 1 only: config 3's whole job (this many clusters) of the headline test and "
+                         "of its crash variant, each on this one GPU as consecutive resident chunks "
+                         "(0 = skip)")
     ap.add_argument("--cpu-seeds", type=int, default=320000,
                     help="cpu_baseline sample: seeds in total, split over one process per core")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -285,6 +289,23 @@ def main():
             "pass_rate": round(sv["passed"] / max(sv["done"], 1), 6),
             "note": "config 3 read literally: crash1/start1 + persister (tests.rs:612-660) in "
                     "figure_8_unreliable's loop"}}
+    if world == 1 and a.million:
+        # config 3 read at full size on ONE GPU (BASELINE.json configs[2]: 1M clusters, which the
+        # driver's 8-GPU run shards 131,072 per GPU): the whole job as consecutive chunks of the
+        # resident capacity, headline test and its crash-restart + persister variant. The on-hardware
+        # stand-in for the 8-GPU total; one untimed warmup job, then one timed job each
+        out.setdefault("variants", {})
+        for t in (a.test, "figure_8_unreliable_crash"):
+            bm = sim.Batch(t, a.million, _abi.README_SEED, device=local, safety=not a.no_safety)
+            em, accm = time_steps(bm, _abi.README_SEED + 7 * a.million, a.million, 1, 1, barrier)
+            bm.close()
+            sm = summed(accm)
+            out["variants"][f"{t}@{a.million}"] = {
+                "value": round(a.million / em, 1), "unit": "seeds/s", "clusters": a.million,
+                "ms_per_job": round(em * 1000, 3), "events_per_sec": round(sm["events"] / em, 1),
+                "events_per_seed": round(sm["events"] / a.million, 1),
+                "pass_rate": round(sm["passed"] / max(sm["done"], 1), 6), "launches": sm["launches"],
+                "note": "config 3's whole job on one MI355X (consecutive resident chunks)"}
     if world == 1 and not a.no_cpu_baseline:  # N = 1 only: the N > 1 lines are scaling points
         # one process per host core this job may use (north_star): the CPUs it may run on, capped
         # by its cgroup CPU quota — on the GPU box 256 CPUs are visible but the quota is 16

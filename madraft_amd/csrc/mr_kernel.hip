@@ -1979,6 +1979,10 @@ __global__ void __launch_bounds__(STEP_BLOCK, step_waves<S>()) step_kernel(Dev D
   static_assert(NBT == NB, "one node bound per translation unit");
   Dev D = Din;
   if constexpr (MR_EXACT_N) D.n = NB;  // the host launches this instance for D.n == NB only
+#ifdef MR_DEV_LEAN  // A/B: test-only features compiled out (bug variants, streaming, traces, null Raft)
+  D.bugs = 0; D.stream = 0; D.trace_clusters = 0; D.null_raft = 0;
+  if constexpr (!is_kv(S)) D.links = 0;
+#endif
   X x;
   // lanes 0 .. lpw - 1 of each 64-lane block hold clusters (D.lpw < 64: a batch smaller than the
   // resident lanes still spreads over two waves per SIMD; the other lanes idle)

@@ -226,13 +226,16 @@ def test_baseline_sizes(hip, oracle, test, clusters, kw):
         assert (oc[0], ot[0], od[0]) == (code[k], t[k], dig[k]), (test, int(k))
 
 
-def test_config3_one_million_on_one_gpu(hip, oracle):
+@pytest.mark.parametrize("test", ["figure_8_unreliable_2c", "figure_8_unreliable_crash"])
+def test_config3_one_million_on_one_gpu(hip, oracle, test):
     """BASELINE config 3's whole job — 1,048,576 clusters of figure_8_unreliable_2c, which the
-    driver shards over 8 GPUs (131,072 each) — run on ONE MI355X as consecutive chunks of the
-    resident capacity: every cluster reaches a verdict, no simulator capacity
-    is hit, and 64 sampled clusters equal the oracle (verdict, time, trace digest)."""
+    driver shards over 8 GPUs (131,072 each), and config 3 read literally (crash1 / start1 +
+    persister, tests.rs:612-660, in figure_8_unreliable's loop) — run on ONE MI355X as
+    consecutive chunks of the resident capacity: every cluster reaches a
+    verdict, no simulator capacity is hit, and 64 sampled clusters equal the oracle (verdict,
+    time, trace digest)."""
     n = 1 << 20
-    with hip.Batch("figure_8_unreliable_2c", n, safety=True) as b:
+    with hip.Batch(test, n, safety=True) as b:
         st = b.run()
         code, t, dig = b.verdicts()
         cnt = b.counters()
@@ -264,15 +267,17 @@ def test_safety_checks_bit_exact(hip, oracle, test, flags):
         assert not np.isin(code, [42, 43, 49]).any()
 
 
-@pytest.mark.parametrize("test,kw", [
-    ("figure_8_unreliable_2c", dict(flags=_abi.MR_F_BUG_VOTE_STALE)),
-    ("figure_8_unreliable_2c", dict(flags=_abi.MR_F_BUG_NO_PREV_CHECK)),
-    ("snapshot_install_unreliable_2d", dict(flags=_abi.MR_F_BUG_VOTE_STALE)),
-    ("snapshot_install_unreliable_2d", dict(flags=_abi.MR_F_BUG_VOTE_TWICE, nodes=7)),
-    ("figure_8_unreliable_2c", dict(apply_cap=64)),
-    ("snapshot_basic_2d", dict(apply_cap=40)),
+# floor: the oracle's count on these 256 seeds when written (246 / 256 / 256 / 24 / 256 / 256),
+# rounded down, so a checker weakened on both sides at once still fails the test
+@pytest.mark.parametrize("test,kw,floor", [
+    ("figure_8_unreliable_2c", dict(flags=_abi.MR_F_BUG_VOTE_STALE), 200),
+    ("figure_8_unreliable_2c", dict(flags=_abi.MR_F_BUG_NO_PREV_CHECK), 200),
+    ("snapshot_install_unreliable_2d", dict(flags=_abi.MR_F_BUG_VOTE_STALE), 200),
+    ("snapshot_install_unreliable_2d", dict(flags=_abi.MR_F_BUG_VOTE_TWICE, nodes=7), 20),
+    ("figure_8_unreliable_2c", dict(apply_cap=64), 200),
+    ("snapshot_basic_2d", dict(apply_cap=40), 200),
 ])
-def test_apply_checker_failures_bit_exact(hip, oracle, test, kw):
+def test_apply_checker_failures_bit_exact(hip, oracle, test, kw, floor):
     """The tester's apply checker (push_and_check, tester.rs:366-396) failing inside the
     cooperative applier (entries of one cluster spread over the wave's lanes): buggy Rafts
     without MR_F_SAFETY commit diverging entries (APPLY_MISMATCH), a tiny apply_cap trips
@@ -282,23 +287,24 @@ def test_apply_checker_failures_bit_exact(hip, oracle, test, kw):
     # the bar is the oracle's own count on these seeds (compare() already made every verdict
     # equal): the checker must have caught something for the test to mean anything
     caught = int(np.isin(ocode, [8, 9, 60]).sum())
-    assert caught >= 1 and int(np.isin(code, [8, 9, 60]).sum()) == caught
+    assert caught >= floor and int(np.isin(code, [8, 9, 60]).sum()) == caught
 
 
-@pytest.mark.parametrize("test,flags", [
-    ("unreliable_3a", _abi.MR_F_BUG_NO_DEDUP),
-    ("unreliable_one_key_3a", _abi.MR_F_BUG_NO_DEDUP),
-    ("persist_partition_unreliable_3a", _abi.MR_F_BUG_STALE_READ),
-    ("many_partitions_many_clients_3a", _abi.MR_F_BUG_STALE_READ),
-    ("persist_partition_unreliable_linearizable_3a", _abi.MR_F_BUG_NO_DEDUP),
-    ("persist_partition_unreliable_linearizable_3a", _abi.MR_F_BUG_STALE_READ),
+# floor: the oracle's count on these 256 seeds when written (256 / 256 / 255 / 76 / 256 / 121)
+@pytest.mark.parametrize("test,flags,floor", [
+    ("unreliable_3a", _abi.MR_F_BUG_NO_DEDUP, 200),
+    ("unreliable_one_key_3a", _abi.MR_F_BUG_NO_DEDUP, 200),
+    ("persist_partition_unreliable_3a", _abi.MR_F_BUG_STALE_READ, 200),
+    ("many_partitions_many_clients_3a", _abi.MR_F_BUG_STALE_READ, 60),
+    ("persist_partition_unreliable_linearizable_3a", _abi.MR_F_BUG_NO_DEDUP, 200),
+    ("persist_partition_unreliable_linearizable_3a", _abi.MR_F_BUG_STALE_READ, 100),
 ])
-def test_linearizability_checker_bit_exact(hip, oracle, test, flags):
+def test_linearizability_checker_bit_exact(hip, oracle, test, flags, floor):
     """SEMANTICS §9a on the GPU: the buggy kvraft servers are caught at the same Get, at the
     same virtual time, with the same traces and counters as the oracle."""
     code, cnt, ocode = compare(hip, oracle, test, 256, oracle_codes=True, flags=flags)
     caught = int((ocode == 52).sum())  # the oracle's own count on these seeds is the bar
-    assert caught >= 1 and int((code == 52).sum()) == caught and cnt["kv_lin_checked"] > 0
+    assert caught >= floor and int((code == 52).sum()) == caught and cnt["kv_lin_checked"] > 0
 
 
 @pytest.mark.parametrize("test", ["figure_8_unreliable_2c", "unreliable_3a"])

@@ -8,7 +8,9 @@ node's role / term / commit / applied / last / snapshot index), and hold for any
 * election safety: at most one node is leader in a term;
 * snapshot <= applied <= commit <= last on a live node;
 * without crashes, a node's commit and applied indices never decrease, and its snapshot index
-  never decreases either way.
+  never decreases either way;
+* leader completeness: a new leader's log reaches every index committed before its election;
+* commit quorum: every committed index is within the logs of a majority (check_commit_quorum).
 
 CPU: oracle traces of many seeds over the BASELINE shapes; GPU: the HIP path's own traces.
 """
@@ -22,7 +24,39 @@ NO_CRASH = {"figure_8_unreliable_2c", "fail_agree_2b", "basic_agree_2b", "unreli
             "snapshot_install_unreliable_2d", "many_partitions_many_clients_3a"}
 
 
-def check_trace(tr, test):
+def check_commit_quorum(tr, n):
+    """Leader completeness and the commit quorum, from the traced indices alone (Raft paper
+    Figure 3; tester.rs:366-428 checks the same entries by value):
+
+    * a node that becomes leader at time t holds every entry committed before t: its last
+      index is at least the largest commit index any node reported before t;
+    * a committed entry is on a majority: at every event the largest commit index reported so
+      far is at most the majority-th largest last index the nodes last reported.
+
+    A node's traced last can lag its true one only by start() appends on a leader (tester
+    events), which only add entries, so both checks hold for a correct Raft on traced values."""
+    maj = n // 2 + 1
+    last = np.zeros(n, np.int64)
+    cmax, prev_t, cmax_before = 0, -1, 0
+    lead_term = {}
+    node = tr[(tr["cls"] <= 1) & (tr["node"] < n)]
+    for ev in node:
+        t = int(ev["time_us"])
+        if t != prev_t:  # commits reported strictly before this time
+            cmax_before, prev_t = cmax, t
+        d, term = int(ev["node"]), int(ev["term"])
+        last[d] = int(ev["last"])
+        if ev["role"] == R_L and term not in lead_term:
+            lead_term[term] = d
+            assert last[d] >= cmax_before, \
+                f"leader {d} of term {term} at t={t} lacks committed index {cmax_before} (last {last[d]})"
+        if ev["role"] != R_DOWN:
+            cmax = max(cmax, int(ev["commit"]))
+        assert np.sort(last)[::-1][maj - 1] >= cmax, \
+            f"t={t}: index {cmax} committed but on fewer than {maj} logs: {last.tolist()}"
+
+
+def check_trace(tr, test, n=None):
     assert (np.diff(tr["time_us"].astype(np.int64)) >= 0).all(), "time went back"
     node = tr[(tr["cls"] <= 1) & (tr["node"] < 8)]  # node events (messages, timers)
     leaders = {}
@@ -39,6 +73,8 @@ def check_trace(tr, test):
             assert (np.diff(r["applied"].astype(np.int64)) >= 0).all(), f"node {d}: applied went back"
         for t in np.unique(r["term"][r["role"] == R_L]):
             assert leaders.setdefault(int(t), int(d)) == int(d), f"two leaders in term {t}"
+    if n:
+        check_commit_quorum(tr, n)
     return len(leaders)
 
 
@@ -55,7 +91,7 @@ def test_oracle_traces_hold_raft_properties(oracle, test, kw):
         cfg = oracle.cfg(test, **kw)
         r, tr = oracle.run_cluster(cfg, c, trace_cap=1 << 17)
         assert tr[-1]["cls"] == 3 and tr[-1]["kind"] == r["code"], "trace truncated"
-        terms += check_trace(tr, test)
+        terms += check_trace(tr, test, int(cfg.n_nodes))
     assert terms > 24  # leaders were elected: the properties had something to hold for
 
 
@@ -69,20 +105,51 @@ def test_gpu_traces_hold_raft_properties(hip, test, kw):
     with hip.Batch(test, 64, trace_clusters=16, trace_cap=1 << 17, **kw) as b:
         b.run()
         traces = [b.trace(k) for k in range(16)]
+        n = int(b.cfg.n_nodes)
     assert all(tr[-1]["cls"] == 3 for tr in traces)  # complete: each ends with its verdict
-    assert sum(check_trace(tr, test) for tr in traces) > 16
+    assert sum(check_trace(tr, test, n) for tr in traces) > 16
 
 
-@pytest.mark.parametrize("test,bug", [("many_election_2a", _abi.MR_F_BUG_VOTE_TWICE),
-                                      ("figure_8_unreliable_2c", _abi.MR_F_BUG_VOTE_STALE)])
-def test_trace_properties_catch_buggy_raft(oracle, test, bug):
+@pytest.mark.gpu
+@pytest.mark.parametrize("test,clusters,kw", [
+    ("figure_8_unreliable_2c", 131072, dict(safety=True)),     # config 3, one GPU's shard
+    ("figure_8_unreliable_crash", 131072, dict(safety=True)),  # ... crash-restart + persister
+    ("snapshot_install_unreliable_2d", 262144, dict(nodes=7)),  # config 4
+])
+def test_gpu_traces_at_baseline_size(hip, test, clusters, kw):
+    """The same properties on traces taken from a BASELINE-size run: 48 clusters spread over
+    the batch (cluster_base shards of the full job, each traced whole) keep every property."""
+    terms = 0
+    for first in (0, clusters // 2, clusters - 16):
+        with hip.Batch(test, 16 if first else clusters, cluster_base=first, trace_clusters=16,
+                       trace_cap=1 << 17, **kw) as b:
+            b.run()
+            traces = [b.trace(k) for k in range(16)]
+            n = int(b.cfg.n_nodes)
+        assert all(tr[-1]["cls"] == 3 for tr in traces)
+        terms += sum(check_trace(tr, test, n) for tr in traces)
+    assert terms > 48
+
+
+@pytest.mark.parametrize("test,bug,check,floor", [
+    ("many_election_2a", _abi.MR_F_BUG_VOTE_TWICE, "all", 20),
+    ("figure_8_unreliable_2c", _abi.MR_F_BUG_VOTE_STALE, "all", 20),
+    ("figure_8_unreliable_2c", _abi.MR_F_BUG_VOTE_STALE, "quorum", 10),
+    ("figure_8_2c", _abi.MR_F_BUG_VOTE_STALE, "quorum", 20)])
+def test_trace_properties_catch_buggy_raft(oracle, test, bug, check, floor):
     """The trace checks are not vacuous: a Raft that votes twice in a term (or for a stale
-    log) elects two leaders in one term on some seeds, and the trace alone shows it."""
+    log) elects two leaders in one term on some seeds, and one that votes for a stale log
+    elects leaders that lack committed entries (leader completeness); the traces alone show it
+    (counts over 64 seeds: 45 / 40 / 26 / 32 when written, floors below them)."""
     caught = 0
     for c in range(64):
-        _, tr = oracle.run_cluster(oracle.cfg(test, flags=bug), c, trace_cap=1 << 17)
+        cfg = oracle.cfg(test, flags=bug)
+        _, tr = oracle.run_cluster(cfg, c, trace_cap=1 << 17)
         try:
-            check_trace(tr, test)
+            if check == "quorum":
+                check_commit_quorum(tr, int(cfg.n_nodes))
+            else:
+                check_trace(tr, test, int(cfg.n_nodes))
         except AssertionError:
             caught += 1
-    assert caught >= 1
+    assert caught >= floor

@@ -18,3 +18,25 @@ for r in $(seq 1 ${ROUNDS:-2}); do
     done
   done
 done
+if [ -n "$PMC" ]; then  # one counter pass per variant: issued instructions, divergence, waits
+  cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+  for f in "$@"; do
+    MADRAFT_HIP_LIB=$V/$f.so timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_VALU SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_WAVE_CYCLES SQ_BUSY_CYCLES --kernel-trace --output-format csv -d $O/pmc_$f -o run -- python3 bench.py --no-cpu-baseline --variant= --steps 1 --warmup 0 > $O/pmc_$f.log 2>&1 || { echo "PMC FAIL $f"; tail -3 $O/pmc_$f.log; exit 1; }
+    python - "$O/pmc_$f" "$f" <<'PY' | tee -a $O/summary.txt
+import csv, glob, sys, collections, json
+a = collections.defaultdict(float)
+for p in glob.glob(sys.argv[1] + "/**/run_counter_collection.csv", recursive=True):
+    for r in csv.DictReader(open(p)):
+        if "step_kernel" in r["Kernel_Name"]:
+            a[r["Counter_Name"]] += float(r["Counter_Value"])
+ev = None
+for line in open(sys.argv[1] + ".log"):
+    if line.startswith("{"):
+        d = json.loads(line); ev = d["events_per_seed"] * d["config"]["clusters_total"]
+print(sys.argv[2], "VALU/ev %.2f SALU/ev %.2f lanes/VALU %.2f wait %.3f active %.3f" % (
+    a["SQ_INSTS_VALU"] / ev, a["SQ_INSTS_SALU"] / ev, a["SQ_THREAD_CYCLES_VALU"] / a["SQ_ACTIVE_INST_VALU"],
+    a["SQ_WAIT_ANY"] / a["SQ_WAVE_CYCLES"], a["SQ_ACTIVE_INST_ANY"] / a["SQ_WAVE_CYCLES"]))
+PY
+  done
+fi
+
