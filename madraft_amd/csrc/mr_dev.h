@@ -93,7 +93,7 @@ enum : uint32_t { KV_GET = 0, KV_PUT = 1, KV_APPEND = 2 };
 enum : uint32_t { KV_OK = 0, KV_WRONG_LEADER = 1, KV_FAILED = 2 };
 constexpr uint32_t CLERK_HOST = 8;  // clerk c is host 8 + c
 constexpr uint32_t KV_PEND = 8;     // pending requests per server
-// kt32 [KT__N][nthr(S)][C]: a spawned tester thread (+ its clerk, kvraft) per slot.
+// kt32 [C][nthr(S)][KT_STRIDE]: a spawned tester thread (+ its clerk, kvraft) per slot.
 // Words KT_W.. are the thread's own frame: kvraft clerk fields, churn client
 // (x lo/hi, index, timeout step, values), or a one() task (helper frame h[0..4], cmd).
 enum : uint32_t {
@@ -112,6 +112,7 @@ enum : uint32_t {
   KT__N
 };
 constexpr uint32_t KT_W = KT_ID;
+constexpr uint32_t KT_STRIDE = (KT__N + 3u) & ~3u;  // words per thread-slot record (16-B multiple)
 constexpr uint32_t JOIN_ALL = 0xFFFFFFFEu;
 constexpr uint32_t JOIN_ANY = 0xFFFFFFFDu;  // select! over spawned tasks: the first finish wakes
 // kvraft key ids / Put value tokens of the test bodies (SEMANTICS §9)
@@ -174,7 +175,7 @@ struct Dev {
   LE* log;  // [C][n][log_cap] ring per node
   LE* pay;  // [C][M][K] AppendEntries payload per message slot
   SE* stor;         // [C][apply_cap]   tester storage (tester.rs:366-428)
-  uint32_t* kt32;   // [KT__N][nthr][C]     (spawning scenarios)
+  uint32_t* kt32;   // [C][nthr][KT_STRIDE] (spawning scenarios)
   uint32_t* kv32;   // [C][n][KVREC]        (kvraft only)
   uint32_t* kvs32;  // [C][n][KVS_W]        persisted KV snapshots (maxraftstate)
   uint32_t* kring;  // [C][KV_RING][KRW]    recent KV snapshots by index (maxraftstate)
@@ -203,7 +204,11 @@ struct Dev {
   uint32_t* held_in;    // [L] those clusters (streaming)
   uint32_t* held_out;   // [L] this launch's (index = its remaining[0] count)
   unsigned long long* prof;  // [PROF_SLOTS] wave-cycle profile (MR_PROF builds only)
+  uint4* tfr;       // [C][TF_Q] the tester coroutine frame, one cluster-major 80-B record
 };
+// tester frame record (tester() in mr_kernel.hip): pc | helper << 24, result, locals l[0..7],
+// helper frame h[0..4], u64 argument hv — 17 words in five 16-B quads, loaded and stored whole
+constexpr uint32_t TF_Q = 5;
 constexpr uint32_t PROF_SLOTS = 64;
 // election-safety term bitmap (MR_F_SAFETY): terms 0..LED_TERMS-1; a leader elected in a
 // later term is a simulator limit (MR_FAIL_SIM_CAPACITY); figure_8 peaks at term 177

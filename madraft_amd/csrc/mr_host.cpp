@@ -316,7 +316,7 @@ static int mr_batch_create_impl(const mr_cfg* cfg, mr_batch** out) {
   add(&D.stor, C * cfg->apply_cap);
   // scenario-only arrays: spawned tester threads, kvraft servers, churn values
   D.nthr = nthr(scn);
-  if (D.nthr) add(&D.kt32, (size_t)KT__N * D.nthr * C);
+  if (D.nthr) add(&D.kt32, (size_t)KT_STRIDE * D.nthr * C);
   if (is_svc(scn)) add(&D.kv32, (size_t)KVREC * n * C);
   if (is_kv(scn)) add(&D.lin32, (size_t)KV_KEYS * KV_APP * LINW * C);
   if (kv_gen(scn).maxraft) {
@@ -335,6 +335,7 @@ static int mr_batch_create_impl(const mr_cfg* cfg, mr_batch** out) {
   add(&D.trace, (size_t)D.trace_clusters * D.trace_cap);
   add(&D.remaining, 2);
   add(&D.prof, PROF_SLOTS);
+  add(&D.tfr, (size_t)TF_Q * C);
   size_t total = 0;
   for (auto& it : items) total += (it.bytes + 255) & ~size_t(255);
 

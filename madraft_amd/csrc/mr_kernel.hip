@@ -498,7 +498,26 @@ DI void rescan_min(const Dev& D, X& x) {
   }
   uint64_t best = ~0ull;
   uint32_t bs = 0;
-  if constexpr (MR_RESCAN_OCC && MW == 1) {
+#ifndef MR_RESCAN_X4  // A/B: four occupied slots per trip, their LDS reads issued together
+#define MR_RESCAN_X4 0
+#endif
+  if constexpr (MR_RESCAN_X4 && MW == 1) {
+    uint64_t occ = ~x.free_mask[0] & (D.M >= 64 ? ~0ull : ((1ull << D.M) - 1ull));
+    while (occ) {
+      uint32_t s4[4];
+#pragma unroll
+      for (uint32_t q = 0; q < 4; q++) {  // a slot past the last occupied one repeats s4[0]
+        s4[q] = occ ? (uint32_t)__builtin_ctzll(occ) : s4[0];
+        occ &= occ - 1ull;
+      }
+      uint64_t k4[4];
+#pragma unroll
+      for (uint32_t q = 0; q < 4; q++) k4[q] = LK(s4[q]);
+#pragma unroll
+      for (uint32_t q = 0; q < 4; q++)
+        if (k4[q] < best) { best = k4[q]; bs = s4[q]; }
+    }
+  } else if constexpr (MR_RESCAN_OCC && MW == 1) {
     uint64_t occ = ~x.free_mask[0] & (D.M >= 64 ? ~0ull : ((1ull << D.M) - 1ull));
     while (occ) {
       const uint32_t s = (uint32_t)__builtin_ctzll(occ);
@@ -1127,6 +1146,165 @@ DI void ae_load_batch(const Dev& D, const X& x, uint32_t me, const NC& d, uint32
   }
 }
 
+// Cooperative AppendEntries receive (MR_AE_COOP). A catch-up payload carries up to K entries;
+// its receiver used to walk them in batches of AC, one dependent round trip per batch, while the
+// wave's other lanes waited. The first batch is still walked by its receiver (the common
+// heartbeat or short append ends there); the entries after it, of every lane of the wave that
+// reached this point, are spread over all those lanes, one entry per lane per round, exactly as
+// node_apply_coop spreads applies. The order-dependent parts of the walk have closed forms:
+//   * skips form a prefix: the first entry written, f, is the first entry that is past our log
+//     or whose term differs from ours (an LDS atomic min per owner); every entry from f on is
+//     written, so d.last = the last entry written;
+//   * MR_F_SAFETY log matching fails iff a skipped entry (below f) differs in its command: no
+//     entry is written then, as in the walk (it fails at that entry's batch, before any write);
+//   * the capacity check fails at the first index past snap + log_cap: the entries below it are
+//     written, then the cluster stops;
+//   * run starts (le_at): entry i >= f written from the sender's entry whose run starts at rs_s
+//     gets rs_s if rs_s >= index(f) (the run starts within what is written), else the run reaches
+//     below f, where our entry f - 1 matched the sender's, so it continues our run: rs(f - 1);
+//   * the write guard (materialize) runs once, before the writes, if any index written shares a
+//     ring slot with the pending payload range — the walk's first guarded write copies the same
+//     messages (no earlier write of this event touched a referenced slot).
+// The kernel's LDS send staging (free until the send loop) holds the exchange words.
+#ifndef MR_AE_COOP
+#define MR_AE_COOP 1
+#endif
+constexpr uint32_t AE_COOP_REM = 12;  // entries after the first batch an owner may hand out (LDS rows)
+DI void wave_sync_lds() {
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
+DI uint32_t rl(uint32_t v, uint32_t lane) {
+  return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)lane);
+}
+// returns false if the cluster failed (its verdict is set)
+DI bool ae_recv_coop(const Dev& D, X& x, uint32_t me, NC& d, uint32_t src, bool mat, uint32_t slot,
+                     uint32_t ma, uint32_t k, uint32_t jr, uint32_t lrs, uint32_t& tprev,
+                     uint32_t& rsprev, bool& wrote, uint32_t plo, uint32_t phi) {
+  uint32_t* const stg = reinterpret_cast<uint32_t*>(s_keys + D.M * STEP_BLOCK);
+  uint32_t* const fw = stg;                    // row 0: first entry written (j), per owner
+  uint32_t* const bw = stg + STEP_BLOCK;       // row 1: first skipped entry with another command
+  uint32_t* const mw = stg + 4 * STEP_BLOCK;   // rows 4..15: our rs at jr + r (matched entries);
+                                               // pass 2: rows 4 / 5 = rs / term of the last written
+  const uint32_t lane = threadIdx.x;           // one wave per block (static_assert STEP_BLOCK)
+  const uint32_t cnt = k > jr ? k - jr : 0u;
+  // entries from jp on are past our log (index ma + 1 + j > last): never a match
+  const uint32_t jp = d.last - ma;  // prev <= last and ma <= prev (a snapshot skip raises prev)
+  const uint32_t f0 = wrote ? jr : (jp > jr ? (jp < k ? jp : k) : jr);
+  const uint32_t c1 = (cnt && !wrote) ? f0 - jr : 0u;  // entries to compare
+  if (cnt) { fw[lane] = f0; bw[lane] = ~0u; }
+  const uint64_t act = __ballot(1);
+  const uint32_t nh = (uint32_t)__popcll(act);
+  const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(act >> 32),
+                                                 __builtin_amdgcn_mbcnt_lo((uint32_t)act, 0u));
+  // the owner's constant fields, packed for the helpers' readlanes
+  const uint32_t oc_ = x.c, pk_ = (mat ? 1u : 0u) | (slot << 1) | (src << 9) | (me << 14);
+  const uint32_t la_ = d.last, lt_ = d.lastt;
+  // pass 1: compare our entries with the payload's where both exist
+  const uint64_t own1 = __ballot(c1 != 0u);
+  if (own1) {
+    uint32_t total = 0;
+    for (uint64_t m = own1; m; m &= m - 1ull) total += rl(c1, (uint32_t)__builtin_ctzll(m));
+    for (uint32_t w0 = 0; w0 < total; w0 += nh) {
+      const uint32_t w = w0 + rank;
+      uint32_t o = 64u, jx = 0, oc = 0, opk = 0, oma = 0, olast = 0, olastt = 0, olrs = 0, pre = 0;
+      for (uint64_t m = own1; m; m &= m - 1ull) {
+        const uint32_t ol = (uint32_t)__builtin_ctzll(m);
+        const uint32_t c = rl(c1, ol);
+        if (pre < w0 + nh && pre + c > w0) {  // uniform: this owner has items in the round
+          const uint32_t v0 = rl(oc_, ol), v1 = rl(pk_, ol), v2 = rl(ma, ol), v3 = rl(la_, ol),
+                         v4 = rl(lt_, ol), v5 = rl(lrs, ol);
+          if (w >= pre && w < pre + c) {
+            o = ol; jx = w - pre; oc = v0; opk = v1; oma = v2; olast = v3; olastt = v4; olrs = v5;
+          }
+        }
+        pre += c;
+        if (pre >= w0 + nh) break;
+      }
+      if (o < 64u) {
+        const uint32_t j = jr + jx, i = oma + 1u + j, ri = i & (D.log_cap - 1u);
+        const uint32_t ome = opk >> 14, osrc = (opk >> 9) & 31u, oslot = (opk >> 1) & 255u;
+        const LE pe = (opk & 1u) ? D.pay[((size_t)oc * D.M + oslot) * D.K + j]
+                                 : D.log[((size_t)oc * D.n + osrc) * D.log_cap + ri];
+        const LE ow = D.log[((size_t)oc * D.n + ome) * D.log_cap + ri];
+        const uint32_t ot = i == olast ? olastt : ow.term, ors = i == olast ? olrs : ow.rs;
+        if (ot != pe.term) {
+          __hip_atomic_fetch_min(&fw[o], j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+        } else {
+          mw[(j - jr) * STEP_BLOCK + o] = ors;
+          if (D.safety && ow.val != pe.val)
+            __hip_atomic_fetch_min(&bw[o], j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+        }
+      }
+    }
+    wave_sync_lds();
+  }
+  // owners: the first write, the end of the writes, rs(f - 1), the write guard
+  uint32_t f = k, jend = k, fcode = 0, rsf = 0;
+  if (cnt) {
+    f = fw[lane];
+    if (D.safety && bw[lane] < f) { fcode = MR_FAIL_SAFETY_LOG_MATCHING; f = k; }
+    const uint32_t jcap = d.snap + D.log_cap - ma;  // index ma + 1 + jcap fails the capacity check
+    if (!fcode) {
+      jend = k < jcap ? k : jcap;
+      if (jend < f) jend = f;
+      if (k > jcap && f < k) fcode = MR_FAIL_SIM_CAPACITY;  // after the entries below it
+    } else {
+      jend = f;
+    }
+    rsf = f == jr ? rsprev : mw[(f - 1u - jr) * STEP_BLOCK + lane];
+    if (jend > f && x.now <= d.pexp && plo <= phi) {  // guard_log_write over [index(f), index(jend - 1)]
+      const uint32_t a = ma + 1u + f, len = jend - 1u - f, span = phi - plo;
+      const uint32_t u = (a - plo) & (D.log_cap - 1u);
+      if (span >= D.log_cap - 1u || u <= span || u + len >= D.log_cap) materialize(D, x, me, d.pexp);
+    }
+  }
+  // pass 2: the writes (materialize's copies are done: program order within the wave)
+  const uint32_t c2 = jend > f ? jend - f : 0u;
+  const uint64_t own2 = __ballot(c2 != 0u);
+  if (own2) {
+    wave_sync_lds();  // pass 1's LDS words are read: rows 4 / 5 take the last entries written
+    uint32_t total = 0;
+    for (uint64_t m = own2; m; m &= m - 1ull) total += rl(c2, (uint32_t)__builtin_ctzll(m));
+    const uint32_t fe_ = f | (jend << 8);
+    for (uint32_t w0 = 0; w0 < total; w0 += nh) {
+      const uint32_t w = w0 + rank;
+      uint32_t o = 64u, jx = 0, oc = 0, opk = 0, oma = 0, ofe = 0, orsf = 0, pre = 0;
+      for (uint64_t m = own2; m; m &= m - 1ull) {
+        const uint32_t ol = (uint32_t)__builtin_ctzll(m);
+        const uint32_t c = rl(c2, ol);
+        if (pre < w0 + nh && pre + c > w0) {
+          const uint32_t v0 = rl(oc_, ol), v1 = rl(pk_, ol), v2 = rl(ma, ol), v3 = rl(fe_, ol),
+                         v4 = rl(rsf, ol);
+          if (w >= pre && w < pre + c) { o = ol; jx = w - pre; oc = v0; opk = v1; oma = v2; ofe = v3; orsf = v4; }
+        }
+        pre += c;
+        if (pre >= w0 + nh) break;
+      }
+      if (o < 64u) {
+        const uint32_t of = ofe & 255u, j = of + jx, i = oma + 1u + j, ri = i & (D.log_cap - 1u);
+        const uint32_t ome = opk >> 14, osrc = (opk >> 9) & 31u, oslot = (opk >> 1) & 255u;
+        const LE pe = (opk & 1u) ? D.pay[((size_t)oc * D.M + oslot) * D.K + j]
+                                 : D.log[((size_t)oc * D.n + osrc) * D.log_cap + ri];
+        const uint32_t rs = pe.rs >= oma + 1u + of ? pe.rs : orsf;
+        D.log[((size_t)oc * D.n + ome) * D.log_cap + ri] = LE{pe.term, rs, pe.val};
+        if (j + 1u == (ofe >> 8)) { mw[o] = rs; mw[STEP_BLOCK + o] = pe.term; }
+      }
+    }
+    wave_sync_lds();
+  }
+  if (c2) {
+    wrote = true;
+    d.last = ma + jend;
+    rsprev = mw[lane];
+    tprev = d.lastt = mw[STEP_BLOCK + lane];
+    CADD(CNT_LOG_WRITES, c2);
+    CMAX(CNT_MAX_LOG, d.last - d.snap);
+  }
+  if (fcode) { fail(D, x, fcode); return false; }
+  return true;
+}
+
 template <uint32_t S>
 DI void node_event(const Dev& D, X& x, bool is_msg, uint32_t tnode, uint32_t slot,
                    uint32_t seq, NR& nr) {
@@ -1362,7 +1540,10 @@ DI void node_event(const Dev& D, X& x, bool is_msg, uint32_t tnode, uint32_t slo
         uint32_t tprev = tp, rsprev = rsp;  // the entry below the next one written
         bool wrote = false;
         CADD(CNT_SHIPPED, k - j0);  // the payload entries this receiver reads (zero-copy until here)
-        for (uint32_t j = j0; j < k; j += AC) {
+        // MR_AE_COOP: the receiver walks the first batch; the entries after it go to the wave
+        const bool coop = MR_AE_COOP && !MR_TAPE && D.K <= AC + AE_COOP_REM;
+        const uint32_t jw = coop ? (k < j0 + AC ? k : j0 + AC) : k;
+        for (uint32_t j = j0; j < jw; j += AC) {
           if (j != j0) ae_load_batch(D, x, me, d, src, mat, pp, ma, k, j, pe, lt, ov, ors);
           if (D.safety) {  // MR_F_SAFETY log matching: same index and term => same entry
 #if !MR_AE_OWN
@@ -1404,6 +1585,9 @@ DI void node_event(const Dev& D, X& x, bool is_msg, uint32_t tnode, uint32_t slo
             CMAX(CNT_MAX_LOG, i - d.snap);
           }
         }
+        if (coop && !ae_recv_coop(D, x, me, d, src, mat, slot, ma, k, jw, lrs, tprev, rsprev, wrote,
+                                  prange_r.x, prange_r.y))
+          return;
         if (wrote) LRS(me) = rsprev;
         uint32_t lc = ma + k;
         if (mc < lc) lc = mc;
@@ -1738,8 +1922,8 @@ DI uint32_t t_term(const Dev& D, X& x, uint32_t i) {
 // The tester's checks over every server read each record's words as one batch of loads
 // (unrolled over the node bound): a loop that loads server by server is one round trip per
 // server, and one per server index some lane needs (MR_T_BATCH; A/B in DESIGN.md §6.8)
-#ifndef MR_T_BATCH  // (the 8-server instances keep the loops: see MR_T_ONEWALK, mr_tester.inc)
-#define MR_T_BATCH (MR_NB <= 7)
+#ifndef MR_T_BATCH
+#define MR_T_BATCH 1
 #endif
 // the terms of every server (words NF_TERM), 0 past D.n
 DI void t_terms(const Dev& D, X& x, uint32_t (&tm)[NB]) {
@@ -1813,15 +1997,19 @@ DI void tester(const Dev& D, X& x) {
 #ifdef MR_DEV_PRIO
   __builtin_amdgcn_s_setprio(MR_DEV_PRIO);
 #endif
-  uint32_t pcw = CS(CS_TPC);
-  t.pc = pcw & 0xFFFFFFu;
-  t.helper = pcw >> 24;
-  t.res = CS(CS_TRES);
-#pragma unroll
-  for (uint32_t k = 0; k < T_NL; k++) t.l[k] = CS(CS_TL + k);
-#pragma unroll
-  for (uint32_t k = 0; k < T_NH; k++) t.h[k] = CS(CS_TH + k);
-  t.hv = C64(C64_THV);
+  // the frame: one cluster-major 80-B record (mr_dev.h TF_Q), five 16-B loads from one address
+  // instead of 17 cluster-minor words with 17 field bases (which the compiler keeps live in
+  // scalar registers across the step loop)
+  const uint4* fr = D.tfr + (size_t)x.c * TF_Q;
+  const uint4 q0 = fr[0], q1 = fr[1], q2 = fr[2], q3 = fr[3], q4 = fr[4];
+  t.pc = q0.x & 0xFFFFFFu;
+  t.helper = q0.x >> 24;
+  t.res = q0.y;
+  t.l[0] = q0.z; t.l[1] = q0.w; t.l[2] = q1.x; t.l[3] = q1.y;
+  t.l[4] = q1.z; t.l[5] = q1.w; t.l[6] = q2.x; t.l[7] = q2.y;
+  t.h[0] = q2.z; t.h[1] = q2.w; t.h[2] = q3.x; t.h[3] = q3.y; t.h[4] = q3.z;
+  t.hv = ((uint64_t)q4.x << 32) | q3.w;
+  static_assert(T_NL == 8 && T_NH == 5, "tester frame record layout");
 #ifdef MR_DEV_PRIO
   __builtin_amdgcn_s_setprio(0);
 #endif
@@ -1856,13 +2044,12 @@ DI void tester(const Dev& D, X& x) {
     if (target >= INF_T) { fail(D, x, MR_FAIL_SIM_CAPACITY); return; }
     x.twake = (uint32_t)target;
   }
-  CS(CS_TPC) = t.pc | (t.helper << 24);
-  CS(CS_TRES) = t.res;
-#pragma unroll
-  for (uint32_t k = 0; k < T_NL; k++) CS(CS_TL + k) = t.l[k];
-#pragma unroll
-  for (uint32_t k = 0; k < T_NH; k++) CS(CS_TH + k) = t.h[k];
-  C64(C64_THV) = t.hv;
+  uint4* fw = D.tfr + (size_t)x.c * TF_Q;
+  fw[0] = make_uint4(t.pc | (t.helper << 24), t.res, t.l[0], t.l[1]);
+  fw[1] = make_uint4(t.l[2], t.l[3], t.l[4], t.l[5]);
+  fw[2] = make_uint4(t.l[6], t.l[7], t.h[0], t.h[1]);
+  fw[3] = make_uint4(t.h[2], t.h[3], t.h[4], (uint32_t)t.hv);
+  fw[4].x = (uint32_t)(t.hv >> 32);
 }
 
 // ---------------------------------------------------------------- kernels
@@ -1979,9 +2166,27 @@ __global__ void __launch_bounds__(STEP_BLOCK, step_waves<S>()) step_kernel(Dev D
   static_assert(NBT == NB, "one node bound per translation unit");
   Dev D = Din;
   if constexpr (MR_EXACT_N) D.n = NB;  // the host launches this instance for D.n == NB only
+  // configuration the scenario fixes (mr_host.cpp sets the same values): compile-time here, so no
+  // loop-invariant predicate on them is kept in scalar registers across the step loop
+  D.nthr = nthr(S);
+  D.links = kv_gen(S).part ? 1u : 0u;
+  D.lin15 = kv_gen(S).lin ? 1u : 0u;
+  if constexpr (!is_svc(S)) D.kv32 = nullptr;
+  if constexpr (kv_gen(S).maxraft == 0) D.kvs32 = nullptr;
+  if constexpr (is_svc(S)) __builtin_assume(D.kv32 != nullptr);
+  if constexpr (kv_gen(S).maxraft > 0) __builtin_assume(D.kvs32 != nullptr);
 #ifdef MR_DEV_LEAN  // A/B: test-only features compiled out (bug variants, streaming, traces, null Raft)
   D.bugs = 0; D.stream = 0; D.trace_clusters = 0; D.null_raft = 0;
   if constexpr (!is_kv(S)) D.links = 0;
+#endif
+#ifdef MR_DEV_NOSTREAM
+  D.stream = 0;
+#endif
+#ifdef MR_DEV_NOBUGS
+  D.bugs = 0;
+#endif
+#ifdef MR_DEV_NOTRACE
+  D.trace_clusters = 0;
 #endif
   X x;
   // lanes 0 .. lpw - 1 of each 64-lane block hold clusters (D.lpw < 64: a batch smaller than the
@@ -2153,6 +2358,7 @@ __global__ void __launch_bounds__(256) reset_kernel(Dev D) {
   for (uint32_t s = 0; s < D.M; s++) MKEY(s) = ~0ull;
   CS(CS_MJOIN) = 0xFFFFFFFFu;
   CS(CS_CWAKE) = INF_T;
+  for (uint32_t q = 0; q < TF_Q; q++) D.tfr[(size_t)x.c * TF_Q + q] = make_uint4(0u, 0u, 0u, 0u);
   if (D.kt32) {  // spawned threads: slot 0 = the test body (+ ck, clerk 0); others empty
     for (uint32_t s = 0; s < D.nthr; s++) {
       for (uint32_t f = 0; f < KT__N; f++) KT(f, s) = 0u;

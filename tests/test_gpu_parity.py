@@ -129,6 +129,18 @@ def test_small_capacities_fail_identically(hip, oracle):
     compare(hip, oracle, "figure_8_unreliable_2c", 128, log_cap=64, msg_slots=6, ae_max=2)
 
 
+@pytest.mark.parametrize("kw", [dict(log_cap=32, msg_slots=12), dict(log_cap=64, flags=_abi.MR_F_SAFETY),
+                                dict(flags=_abi.MR_F_SAFETY | _abi.MR_F_BUG_NO_PREV_CHECK)])
+def test_cooperative_append_receive(hip, oracle, kw):
+    """The cooperative AppendEntries receive (MR_AE_COOP: a payload's entries after the first
+    batch spread over the wave): full 16-entry payloads hitting a tiny log ring (SIM_CAPACITY
+    part-way through the spread entries, write-guard materializations), MR_F_SAFETY log
+    matching, and a Raft without the prev check (whose logs diverge) — all equal to the
+    oracle's sequential walk."""
+    code, cnt = compare(hip, oracle, "figure_8_unreliable_2c", 512, traced=3, **kw)
+    assert cnt["log_writes"] > 0
+
+
 def test_step_budget_independence(hip):
     """Results do not depend on how many events one launch processes."""
     with hip.Batch("figure_8_unreliable_2c", 512) as b:
