@@ -301,12 +301,12 @@ static int mr_batch_create_impl(const mr_cfg* cfg, mr_batch** out) {
   };
   // field matrices use 32-bit element offsets in the kernels
   const uint64_t lim = 1ull << 32;
-  if ((uint64_t)CS__N * C >= lim || (uint64_t)C64__N * C >= lim || M * C >= lim) {
+  if ((uint64_t)CS_STRIDE * C >= lim || (uint64_t)C64_STRIDE * C >= lim || M * C >= lim) {
     delete b;
     return set_err("n_clusters too large for one batch (32-bit field offsets)");
   }
-  add(&D.cs32, (size_t)CS__N * C);
-  add(&D.cs64, (size_t)C64__N * C);
+  add(&D.cs32, (size_t)CS_STRIDE * C);
+  add(&D.cs64, (size_t)C64_STRIDE * C);
   add(&D.nd32, (size_t)NREC * n * C);
   add(&D.tmr, n * C);
   add(&D.ms32, (size_t)MREC * M * C);
@@ -561,17 +561,18 @@ static int mr_batch_verdicts_impl(mr_batch* b, uint16_t* code, uint32_t* time_us
   HIPCHK(hipSetDevice(b->cfg.device));
   size_t C = b->D.C;
   std::vector<uint32_t> c32;
+  // one field of every cluster: a strided row (cluster-major records) or a contiguous one
+  auto row = [&](void* dst, const void* base, size_t f, size_t width, bool wide) -> hipError_t {
+    const char* p = static_cast<const char*>(base) + (wide ? C64_IDX(f, 0, C) : CS_IDX(f, 0, C)) * width;
+    const size_t pitch = (wide ? C64_IDX(f, 1, C) - C64_IDX(f, 0, C) : CS_IDX(f, 1, C) - CS_IDX(f, 0, C)) * width;
+    return hipMemcpy2DAsync(dst, width, p, pitch, width, C, hipMemcpyDeviceToHost, b->stream);
+  };
   if (code) {
     c32.resize(C);
-    HIPCHK(hipMemcpyAsync(c32.data(), b->D.cs32 + (size_t)CS_CODE * C, C * 4,
-                          hipMemcpyDeviceToHost, b->stream));
+    HIPCHK(row(c32.data(), b->D.cs32, CS_CODE, 4, false));
   }
-  if (time_us)
-    HIPCHK(hipMemcpyAsync(time_us, b->D.cs32 + (size_t)CS_VTIME * C, C * 4, hipMemcpyDeviceToHost,
-                          b->stream));
-  if (digest)
-    HIPCHK(hipMemcpyAsync(digest, b->D.cs64 + (size_t)C64_DIGEST * C, C * 8,
-                          hipMemcpyDeviceToHost, b->stream));
+  if (time_us) HIPCHK(row(time_us, b->D.cs32, CS_VTIME, 4, false));
+  if (digest) HIPCHK(row(digest, b->D.cs64, C64_DIGEST, 8, true));
   HIPCHK(hipStreamSynchronize(b->stream));
   for (size_t i = 0; i < c32.size(); i++) code[i] = (uint16_t)c32[i];
   return 0;
@@ -613,7 +614,7 @@ int mr_batch_counters(mr_batch* b, mr_counters* out) {
   if (out->first_fail_cluster != ~0ull) {
     uint32_t code = 0;
     size_t idx = out->first_fail_cluster - b->cfg.cluster_base;
-    HIPCHK(hipMemcpy(&code, b->D.cs32 + (size_t)CS_CODE * b->D.C + idx, 4, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(&code, b->D.cs32 + CS_IDX(CS_CODE, idx, b->D.C), 4, hipMemcpyDeviceToHost));
     out->first_fail_code = code;
   }
   return 0;
@@ -624,7 +625,7 @@ int mr_trace_get(mr_batch* b, uint32_t k, mr_event* out, size_t cap, size_t* n) 
   if (k >= b->D.trace_clusters) return set_err("cluster not traced");
   HIPCHK(hipSetDevice(b->cfg.device));
   uint32_t tn = 0;
-  HIPCHK(hipMemcpy(&tn, b->D.cs32 + (size_t)CS_TRACEN * b->D.C + k, 4, hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(&tn, b->D.cs32 + CS_IDX(CS_TRACEN, k, b->D.C), 4, hipMemcpyDeviceToHost));
   size_t m = tn < b->D.trace_cap ? tn : b->D.trace_cap;
   if (m > cap) m = cap;
   HIPCHK(hipMemcpy(out, b->D.trace + (size_t)k * b->D.trace_cap, m * sizeof(mr_event),
@@ -718,7 +719,7 @@ static int mr_batch_get_decisions_impl(mr_batch* b, uint32_t k, mr_decision* out
   HIPCHK(hipSetDevice(b->cfg.device));
   HIPCHK(hipStreamSynchronize(b->stream));
   uint32_t used = 0;
-  HIPCHK(hipMemcpy(&used, b->D.cs32 + (size_t)CS_TAPE * b->D.C + k, 4, hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(&used, b->D.cs32 + CS_IDX(CS_TAPE, k, b->D.C), 4, hipMemcpyDeviceToHost));
   *n = used;
   if (b->D.tape_mode != 2 || !out) return 0;
   size_t m = used < b->D.dcap ? used : b->D.dcap;

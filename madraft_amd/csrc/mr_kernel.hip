@@ -72,8 +72,8 @@ struct X {
 };
 
 // field accessors (32-bit element offsets, checked at batch creation)
-#define CS(f) D.cs32[(uint32_t)(f) * D.C + x.c]
-#define C64(f) D.cs64[(uint32_t)(f) * D.C + x.c]
+#define CS(f) D.cs32[CS_IDX(f, x.c, D.C)]
+#define C64(f) D.cs64[C64_IDX(f, x.c, D.C)]
 #define NDP(d) (D.nd32 + ((size_t)x.c * D.n + (d)) * NREC)  // node d's 128-B record
 #define ND(f, d) NDP(d)[f]
 #define NSV(d) (*reinterpret_cast<uint64_t*>(NDP(d) + NF_SNAPV))
@@ -1198,7 +1198,7 @@ DI bool ae_recv_coop(const Dev& D, X& x, uint32_t me, NC& d, uint32_t src, bool 
   const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(act >> 32),
                                                  __builtin_amdgcn_mbcnt_lo((uint32_t)act, 0u));
   // the owner's constant fields, packed for the helpers' readlanes
-  const uint32_t oc_ = x.c, pk_ = (mat ? 1u : 0u) | (slot << 1) | (src << 9) | (me << 14);
+  const uint32_t oc_ = x.c, pk_ = (mat ? 1u : 0u) | (slot << 1) | (src << 9) | (me << 14) | (jr << 20);
   const uint32_t la_ = d.last, lt_ = d.lastt;
   // pass 1: compare our entries with the payload's where both exist
   const uint64_t own1 = __ballot(c1 != 0u);
@@ -1222,8 +1222,9 @@ DI bool ae_recv_coop(const Dev& D, X& x, uint32_t me, NC& d, uint32_t src, bool 
         if (pre >= w0 + nh) break;
       }
       if (o < 64u) {
-        const uint32_t j = jr + jx, i = oma + 1u + j, ri = i & (D.log_cap - 1u);
-        const uint32_t ome = opk >> 14, osrc = (opk >> 9) & 31u, oslot = (opk >> 1) & 255u;
+        // the owner's jr (a helper's own first-batch end differs when its payload is shorter)
+        const uint32_t ojr = opk >> 20, j = ojr + jx, i = oma + 1u + j, ri = i & (D.log_cap - 1u);
+        const uint32_t ome = (opk >> 14) & 7u, osrc = (opk >> 9) & 31u, oslot = (opk >> 1) & 255u;
         const LE pe = (opk & 1u) ? D.pay[((size_t)oc * D.M + oslot) * D.K + j]
                                  : D.log[((size_t)oc * D.n + osrc) * D.log_cap + ri];
         const LE ow = D.log[((size_t)oc * D.n + ome) * D.log_cap + ri];
@@ -1231,7 +1232,7 @@ DI bool ae_recv_coop(const Dev& D, X& x, uint32_t me, NC& d, uint32_t src, bool 
         if (ot != pe.term) {
           __hip_atomic_fetch_min(&fw[o], j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
         } else {
-          mw[(j - jr) * STEP_BLOCK + o] = ors;
+          mw[jx * STEP_BLOCK + o] = ors;
           if (D.safety && ow.val != pe.val)
             __hip_atomic_fetch_min(&bw[o], j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
         }
@@ -1283,7 +1284,7 @@ DI bool ae_recv_coop(const Dev& D, X& x, uint32_t me, NC& d, uint32_t src, bool 
       }
       if (o < 64u) {
         const uint32_t of = ofe & 255u, j = of + jx, i = oma + 1u + j, ri = i & (D.log_cap - 1u);
-        const uint32_t ome = opk >> 14, osrc = (opk >> 9) & 31u, oslot = (opk >> 1) & 255u;
+        const uint32_t ome = (opk >> 14) & 7u, osrc = (opk >> 9) & 31u, oslot = (opk >> 1) & 255u;
         const LE pe = (opk & 1u) ? D.pay[((size_t)oc * D.M + oslot) * D.K + j]
                                  : D.log[((size_t)oc * D.n + osrc) * D.log_cap + ri];
         const uint32_t rs = pe.rs >= oma + 1u + of ? pe.rs : orsf;
@@ -1543,7 +1544,21 @@ DI void node_event(const Dev& D, X& x, bool is_msg, uint32_t tnode, uint32_t slo
         // MR_AE_COOP: the receiver walks the first batch; the entries after it go to the wave
         const bool coop = MR_AE_COOP && !MR_TAPE && D.K <= AC + AE_COOP_REM;
         const uint32_t jw = coop ? (k < j0 + AC ? k : j0 + AC) : k;
+#ifdef MR_DEV_AEDBG  // debug: lanes whose rest needs comparisons (MR_DEV_AEDBG 1) or all (2) walk it
+        for (uint32_t pass = 0; pass < 2; pass++) {
+        uint32_t kc = k;
+        if (pass == 1 && coop) {
+          const bool cmp = !wrote && d.last - ma > jw;
+          kc = (MR_DEV_AEDBG == 2 || cmp) ? jw : k;
+          if (!ae_recv_coop(D, x, me, d, src, mat, slot, ma, kc, jw, lrs, tprev, rsprev, wrote,
+                            prange_r.x, prange_r.y))
+            return;
+        }
+        const uint32_t ja = pass == 0 ? j0 : (coop && kc < k ? jw : k), jb = pass == 0 ? jw : k;
+        for (uint32_t j = ja; j < jb; j += AC) {
+#else
         for (uint32_t j = j0; j < jw; j += AC) {
+#endif
           if (j != j0) ae_load_batch(D, x, me, d, src, mat, pp, ma, k, j, pe, lt, ov, ors);
           if (D.safety) {  // MR_F_SAFETY log matching: same index and term => same entry
 #if !MR_AE_OWN
@@ -1585,9 +1600,13 @@ DI void node_event(const Dev& D, X& x, bool is_msg, uint32_t tnode, uint32_t slo
             CMAX(CNT_MAX_LOG, i - d.snap);
           }
         }
+#ifdef MR_DEV_AEDBG
+        }
+#else
         if (coop && !ae_recv_coop(D, x, me, d, src, mat, slot, ma, k, jw, lrs, tprev, rsprev, wrote,
                                   prange_r.x, prange_r.y))
           return;
+#endif
         if (wrote) LRS(me) = rsprev;
         uint32_t lc = ma + k;
         if (mc < lc) lc = mc;

@@ -98,3 +98,19 @@ def test_bad_config_is_an_error_not_a_crash(L):
     cfg.log_cap = 1000
     with pytest.raises(sim.SimError, match="log_cap"):
         sim.Batch(cfg=cfg)
+
+
+def test_build_instance_tables_match_the_kernels():
+    """build.py compiles the exact-size step-kernel instances mr_dev.h's has_exact() names (the
+    host dispatches to them): the scenarios' default server counts and the 7-server set agree."""
+    dev = open(os.path.join(ROOT, "madraft_amd", "csrc", "mr_dev.h")).read()
+    body = re.search(r"k_default_n\[\]\s*=\s*\{([^}]*)\}", dev).group(1)
+    assert [int(v) for v in body.replace("\n", " ").split(",")] == build.DEFAULT_N
+    lo, hi = re.search(r"has_nb7\(uint32_t s\) \{\s*return s >= (\w+) && s <= (\w+);", dev).groups()
+    hdr = open(HEADER).read()
+    ids = {m.group(1): int(m.group(2)) for m in re.finditer(r"(MR_SCN_\w+) = (\d+)", hdr)}
+    assert set(range(ids[lo], ids[hi] + 1)) == build.NB7_SCNS
+    assert ids["MR_SCN_FAIL_AGREE_2B"] == 5 and build.has_exact(5, 5)  # BASELINE config 2
+    for i in build.SCN_IDS:
+        assert build.has_exact(i, build.DEFAULT_N[i]) == (build.DEFAULT_N[i] < 8)
+        assert not build.has_exact(i, 8)

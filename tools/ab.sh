@@ -7,13 +7,15 @@ V=$PWD/madraft_amd/lib/var
 TESTS=${TESTS:-figure_8_unreliable_2c}
 PTEST=${PTEST:-"test_scenario_bit_exact and (figure_8_unreliable_2c or figure_8_unreliable_crash)"}
 for f in "$@"; do
-  MADRAFT_HIP_LIB=$V/$f.so timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 120 --timeout-method thread -k "$PTEST" > $O/parity_$f.log 2>&1 || { echo "PARITY FAIL $f"; tail -15 $O/parity_$f.log; exit 1; }
+  case " $NOPAR " in *" $f "*) echo "$f parity: skipped (timing-only variant)"; continue;; esac
+  if [ -n "$PIDS" ]; then PSEL="$PIDS"; else PSEL="tests/test_gpu_parity.py -k"; fi
+  MADRAFT_HIP_LIB=$V/$f.so timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread $PSEL "$PTEST" > $O/parity_$f.log 2>&1 || { echo "PARITY FAIL $f"; tail -15 $O/parity_$f.log; exit 1; }
   echo "$f parity: $(tail -1 $O/parity_$f.log)"
 done
 for r in $(seq 1 ${ROUNDS:-2}); do
   for t in $TESTS; do
     for f in "$@"; do
-      MADRAFT_HIP_LIB=$V/$f.so timeout -k 10 300 python bench.py --test $t --steps ${STEPS:-3} --warmup 1 --no-cpu-baseline --variant '' $BARGS > $O/b_${t}_$f.json 2> $O/b_${t}_$f.err || { echo "BENCH FAIL $f $t"; tail -5 $O/b_${t}_$f.err; exit 1; }
+      MADRAFT_HIP_LIB=$V/$f.so timeout -k 10 300 python bench.py --test $t --steps ${STEPS:-3} --warmup 1 --no-cpu-baseline --variant '' --million 0 $BARGS > $O/b_${t}_$f.json 2> $O/b_${t}_$f.err || { echo "BENCH FAIL $f $t"; tail -5 $O/b_${t}_$f.err; exit 1; }
       python -c "import json; d=json.loads(open('$O/b_${t}_$f.json').read().strip().splitlines()[-1]); print('$r $t $f', d['value'], 'ms/launch %.2f' % d['roofline']['avg_launch_ms'], 'ev/seed', d['events_per_seed'])" | tee -a $O/summary.txt
     done
   done
@@ -21,7 +23,7 @@ done
 if [ -n "$PMC" ]; then  # one counter pass per variant: issued instructions, divergence, waits
   cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
   for f in "$@"; do
-    MADRAFT_HIP_LIB=$V/$f.so timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_VALU SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_WAVE_CYCLES SQ_BUSY_CYCLES --kernel-trace --output-format csv -d $O/pmc_$f -o run -- python3 bench.py --no-cpu-baseline --variant= --steps 1 --warmup 0 > $O/pmc_$f.log 2>&1 || { echo "PMC FAIL $f"; tail -3 $O/pmc_$f.log; exit 1; }
+    MADRAFT_HIP_LIB=$V/$f.so timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_VALU SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_WAVE_CYCLES SQ_BUSY_CYCLES --kernel-trace --output-format csv -d $O/pmc_$f -o run -- python3 bench.py --no-cpu-baseline --variant= --million 0 --steps 1 --warmup 0 $BARGS > $O/pmc_$f.log 2>&1 || { echo "PMC FAIL $f"; tail -3 $O/pmc_$f.log; exit 1; }
     python - "$O/pmc_$f" "$f" <<'PY' | tee -a $O/summary.txt
 import csv, glob, sys, collections, json
 a = collections.defaultdict(float)

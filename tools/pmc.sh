@@ -10,5 +10,5 @@ IFS=';' read -ra groups <<< "${PMC_GROUPS:-$DEF}"
 i=0
 for grp in "${groups[@]}"; do
   i=$((i+1))
-  timeout -s KILL 240 rocprofv3 --pmc $grp --kernel-trace --output-format csv -d "$out/p$i" -o run -- python3 bench.py --no-cpu-baseline "$@" > "$out/p$i.log" 2>&1
+  timeout -s KILL 240 rocprofv3 --pmc $grp --kernel-trace --output-format csv -d "$out/p$i" -o run -- python3 bench.py --no-cpu-baseline --million 0 "$@" > "$out/p$i.log" 2>&1
 done
