@@ -1166,8 +1166,12 @@ DI void ae_load_batch(const Dev& D, const X& x, uint32_t me, const NC& d, uint32
 //     ring slot with the pending payload range — the walk's first guarded write copies the same
 //     messages (no earlier write of this event touched a referenced slot).
 // The kernel's LDS send staging (free until the send loop) holds the exchange words.
+// Measured (round 4, same box, profiles/r04_ab_ae_coop.txt): figure_8_unreliable_2c 124.4 -> 125.8 ms,
+// its crash variant -1 %, the 15-clerk linearizable kvraft config +1.4 %; ae_req ticks per visit
+// 570 -> 675 in the section profile (the owner walk's readlanes and the LDS exchange cost more
+// than the batches they replace). Off; kept for the record and for A/B.
 #ifndef MR_AE_COOP
-#define MR_AE_COOP 1
+#define MR_AE_COOP 0
 #endif
 constexpr uint32_t AE_COOP_REM = 12;  // entries after the first batch an owner may hand out (LDS rows)
 DI void wave_sync_lds() {

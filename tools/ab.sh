@@ -8,8 +8,8 @@ TESTS=${TESTS:-figure_8_unreliable_2c}
 PTEST=${PTEST:-"test_scenario_bit_exact and (figure_8_unreliable_2c or figure_8_unreliable_crash)"}
 for f in "$@"; do
   case " $NOPAR " in *" $f "*) echo "$f parity: skipped (timing-only variant)"; continue;; esac
-  if [ -n "$PIDS" ]; then PSEL="$PIDS"; else PSEL="tests/test_gpu_parity.py -k"; fi
-  MADRAFT_HIP_LIB=$V/$f.so timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread $PSEL "$PTEST" > $O/parity_$f.log 2>&1 || { echo "PARITY FAIL $f"; tail -15 $O/parity_$f.log; exit 1; }
+  if [ -n "$PIDS" ]; then set -- "$@"; PARGS=($PIDS); else PARGS=(tests/test_gpu_parity.py -k "$PTEST"); fi
+  MADRAFT_HIP_LIB=$V/$f.so timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread "${PARGS[@]}" > $O/parity_$f.log 2>&1 || { echo "PARITY FAIL $f"; tail -15 $O/parity_$f.log; exit 1; }
   echo "$f parity: $(tail -1 $O/parity_$f.log)"
 done
 for r in $(seq 1 ${ROUNDS:-2}); do

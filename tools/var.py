@@ -30,7 +30,7 @@ def one(spec, scns, csrc=None):
     name, _, flags = spec.partition(":")
     extra = [f for f in flags.split(",") if f]
     out = os.path.join(build.HERE, "lib", "var", name + ".so")
-    build.build_hip(extra=extra, out=out, scns=scns, csrc=csrc)
+    build.build_hip(force=True, extra=extra, out=out, scns=scns, csrc=csrc)
     return out
 
 
