@@ -786,7 +786,17 @@ DI void node_apply(const Dev& D, X& x, uint32_t me, NC& d, bool& kvready) {
     // KV (not the controller): the batch's key records and dedup words as one batch of loads
     // (the batch's commands are known here); an entry whose key or clerk an earlier entry of
     // the batch shares reads them after that entry's stores instead (kv_apply loads)
-    constexpr bool PRE = KV && !is_ctrl(S) && MR_KV_PRE;
+    constexpr bool PRE = KV && !is_ctrl(S) && !kv_gen(S).lin && MR_KV_PRE;
+    // generic_test_linearizability's servers (SEMANTICS §9b): each entry's key-record quad, the
+    // clerk's dedup word and the state word of the client it names, for the whole batch at once
+    // (an entry sharing a key or a clerk with an earlier one of the batch reads them after that
+    // entry's stores instead) — one round trip per batch instead of one per entry. Measured
+    // round 4 (profiles/r04_ab_round4.txt, 65536 clusters): parity-green but 3a 656 -> 712 ms,
+    // 3b 804 -> 807 ms (the batch's 5x6 live words cost more than the round trips they save) — off
+#ifndef MR_LIN15_PRE
+#define MR_LIN15_PRE 0
+#endif
+    constexpr bool PRE15 = KV && !is_ctrl(S) && kv_gen(S).lin && MR_LIN15_PRE;
     uint4 pka[AC_APPLY], pkb[AC_APPLY];
     uint32_t pdd[AC_APPLY], pkey[AC_APPLY], pcl[AC_APPLY];
     if constexpr (PRE) {
@@ -802,6 +812,24 @@ DI void node_apply(const Dev& D, X& x, uint32_t me, NC& d, bool& kvready) {
         const uint4* kq = reinterpret_cast<const uint4*>(kp + KVR_KEYS + KV_KW * key);
         pka[j] = ok ? kq[0] : uint4{};
         pkb[j] = ok ? kq[1] : uint4{};
+        pdd[j] = ok ? kp[KVR_DEDUP + cl] : 0u;
+      }
+    }
+    if constexpr (PRE15) {
+      const uint32_t* kp = KVP(me);
+#pragma unroll
+      for (uint32_t j = 0; j < AC_APPLY; j++) {
+        const uint32_t i = i0 + j;
+        const bool ok = i <= d.commit && i < D.apply_cap;
+        const uint64_t v = ce[j].val;
+        const uint32_t op = (uint32_t)(v >> 61) & 3u, key = (uint32_t)(v >> 55) & 15u;
+        const uint32_t cl = (uint32_t)(v >> 48) & 127u, elem = (uint32_t)v & 0xFFFFFFu;
+        const uint32_t cs = op == KV_GET ? elem : elem >> 19;
+        pkey[j] = ok ? key : 64u + j;  // no match for entries past the batch
+        pcl[j] = ok ? cl : 128u + j;
+        const uint32_t* kr = kp + KVR_KEYS + KV_KW15 * key;
+        pka[j] = ok ? reinterpret_cast<const uint4*>(kr)[0] : uint4{};
+        pkb[j].x = ok && cs < LIN_CLI ? kr[3 + cs] : 0u;
         pdd[j] = ok ? kp[KVR_DEDUP + cl] : 0u;
       }
     }
@@ -828,7 +856,7 @@ DI void node_apply(const Dev& D, X& x, uint32_t me, NC& d, bool& kvready) {
       }
       if constexpr (KV) {
         bool pre = false;
-        if constexpr (PRE) {
+        if constexpr (PRE || PRE15) {
           bool conf = false;
 #pragma unroll
           for (uint32_t q = 0; q < j; q++) conf |= pkey[q] == pkey[j] || pcl[q] == pcl[j];
@@ -1329,7 +1357,17 @@ DI void node_event(const Dev& D, X& x, bool is_msg, uint32_t tnode, uint32_t slo
   const bool has_rec = !KV || me < CLERK_HOST;
   NC d = has_rec ? load_node(D, x, me) : NC{};
   PV pv;
-  if (has_rec) load_peers(D, x, me, pv);
+#ifndef MR_PEERS_LEADER  // next[] / match[] loaded only for a leader's event (A/B round 4)
+#define MR_PEERS_LEADER 1
+#endif
+  // only a leader reads them (appends, acknowledgements); x.lmask mirrors the stored roles
+  // (store_node), so the record's role is known without waiting for it
+  if (has_rec && (!MR_PEERS_LEADER || bit(x.lmask, me))) {
+    load_peers(D, x, me, pv);
+  } else {
+#pragma unroll
+    for (uint32_t q = 0; q < NB; q++) { pv.nx[q] = 0u; pv.mt[q] = 0u; }
+  }
 #if MR_PLO_EARLY
   const uint2 prange = has_rec ? reinterpret_cast<const uint2*>(NDP(me))[NF_PLO / 2] : make_uint2(0u, 0u);
 #else
@@ -1699,10 +1737,19 @@ DI void node_event(const Dev& D, X& x, bool is_msg, uint32_t tnode, uint32_t slo
   // a leader's appends read our terms at next[p] - 1: issue those loads before the applier's
   // checker stores (the ring slot is valid whatever the applier does; gated after it)
   uint32_t rawt[NB];
+#ifndef MR_RAWT_NEED  // only the terms the append will read (A/B round 4)
+#define MR_RAWT_NEED 1
+#endif
+  const uint32_t lbase0 = MR_RAWT_NEED ? sel_nb(pv.mt, me) : 0u;
 #pragma unroll
   for (uint32_t p = 0; p < NB; p++) {
     const uint32_t ix = pv.nx[p] - 1u;
-    rawt[p] = (mode == SEND_APPEND && bit(peers & reach, p) && p < D.n && ix != 0u) ? D.log[logi(D, x, me, ix)].term : 0u;
+    // the append reads the ring only for an index below the leader's base that is neither the
+    // snapshot nor the last entry (LPT below); the applier may raise the snapshot index, which
+    // only turns a load into an InstallSnapshot or a snapshot-term read, never the other way
+    const bool need = !MR_RAWT_NEED || (ix != d.snap && ix != d.last && ix <= lbase0);
+    rawt[p] = (mode == SEND_APPEND && bit(peers & reach, p) && p < D.n && ix != 0u && need)
+                  ? D.log[logi(D, x, me, ix)].term : 0u;
   }
 #endif
   if (MR_AP_COOP && !KV && kv_gen(S).maxraft == 0) {
