@@ -9,6 +9,7 @@ node's role / term / commit / applied / last / snapshot index), and hold for any
 * snapshot <= applied <= commit <= last on a live node;
 * without crashes, a node's commit and applied indices never decrease, and its snapshot index
   never decreases either way;
+* leader append-only: while a node leads in a term, its last index never decreases;
 * leader completeness: a new leader's log reaches every index committed before its election;
 * commit quorum: every committed index is within the logs of a majority (check_commit_quorum).
 
@@ -73,6 +74,9 @@ def check_trace(tr, test, n=None):
             assert (np.diff(r["applied"].astype(np.int64)) >= 0).all(), f"node {d}: applied went back"
         for t in np.unique(r["term"][r["role"] == R_L]):
             assert leaders.setdefault(int(t), int(d)) == int(d), f"two leaders in term {t}"
+            led = r[(r["role"] == R_L) & (r["term"] == t)]
+            assert (np.diff(led["last"].astype(np.int64)) >= 0).all(), \
+                f"node {d}: leader of term {t} removed entries"
     if n:
         check_commit_quorum(tr, n)
     return len(leaders)
