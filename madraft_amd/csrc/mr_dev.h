@@ -111,7 +111,7 @@ constexpr uint32_t KV_PEND = 8;     // pending requests per server
 // Words KT_W.. are the thread's own frame: kvraft clerk fields, churn client
 // (x lo/hi, index, timeout step, values), or a one() task (helper frame h[0..4], cmd).
 enum : uint32_t {
-  KT_TID, KT_LIVE, KT_PC, KT_J, KT_CLI, KT_TCTR, KT_WAKE, KT_ID, KT_LH, KT_SEQ, KT_TAG, KT_NCTR,
+  KT_TID, KT_LIVE, KT_PC, KT_J, KT_CLI, KT_TCTR, KT_WAKE /* unused: kwk */, KT_ID, KT_LH, KT_SEQ, KT_TAG, KT_NCTR,
   KT_WAITING, KT_GOT, KT_RSTAT, KT_RHINT, KT_RVAL, KT_OP, KT_KEY, KT_ELEM,
   KT_KIND,  // 1 = generic_test partitioner (KT_PERM: its shuffled `all`, 4 bits per server)
   KT_PERM,
@@ -219,7 +219,11 @@ struct Dev {
   uint32_t* held_out;   // [L] this launch's (index = its remaining[0] count)
   unsigned long long* prof;  // [PROF_SLOTS] wave-cycle profile (MR_PROF builds only)
   uint4* tfr;       // [C][TF_Q] the tester coroutine frame, one cluster-major 80-B record
+  uint32_t* kwk;    // [C][kws(nthr)][2] thread slots' {tid, wake}: the scheduler's keys, packed
 };
+// words-pairs per cluster of kwk: the thread slots rounded up to whole 16-B quads (two slots each;
+// slot 0 = the test body and the pad slot hold ~0, so they never win a rescan)
+constexpr uint32_t kws(uint32_t nthr) { return (nthr + 1u) & ~1u; }
 // tester frame record (tester() in mr_kernel.hip): pc | helper << 24, result, locals l[0..7],
 // helper frame h[0..4], u64 argument hv — 17 words in five 16-B quads, loaded and stored whole
 constexpr uint32_t TF_Q = 5;

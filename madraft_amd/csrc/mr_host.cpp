@@ -317,6 +317,7 @@ static int mr_batch_create_impl(const mr_cfg* cfg, mr_batch** out) {
   // scenario-only arrays: spawned tester threads, kvraft servers, churn values
   D.nthr = nthr(scn);
   if (D.nthr) add(&D.kt32, (size_t)KT_STRIDE * D.nthr * C);
+  if (D.nthr) add(&D.kwk, (size_t)2 * kws(D.nthr) * C);
   if (is_svc(scn)) add(&D.kv32, (size_t)KVREC * n * C);
   if (is_kv(scn)) add(&D.lin32, (size_t)KV_KEYS * KV_APP * LINW * C);
   if (kv_gen(scn).maxraft) {

@@ -749,7 +749,7 @@ enum : uint32_t { SEND_NONE = 0, SEND_REPLY, SEND_APPEND, SEND_VOTE };
 // whose loads (log entry, storage mask / value) are all issued before any is
 // used — entries have distinct indices, so a batch never reads what it writes.
 template <uint32_t S>
-DI void node_apply(const Dev& D, X& x, uint32_t me, NC& d, bool& kvready) {
+DI void node_apply(const Dev& D, X& x, uint32_t me, NC& d, uint32_t& kvready) {
   constexpr bool KV = is_svc(S);
   const bool snapmode = (x.netmode >> 1) & 1u;
   SE* const sb = D.stor + (size_t)x.c * D.apply_cap;
@@ -1343,7 +1343,7 @@ DI void node_event(const Dev& D, X& x, bool is_msg, uint32_t tnode, uint32_t slo
                    uint32_t seq, NR& nr) {
   constexpr bool KV = is_svc(S);  // kvraft / shard_ctrler request path
   uint32_t me = tnode, src = 0, type = 0, inc = 0, k = 0, mterm = 0, ma = 0, mb = 0, mc = 0;
-  bool kvready = false;
+  uint32_t kvready = 0;  // KV: the pending-request slots answered in this event (kv_flush)
   uint32_t hdr_bits = 0;
 #ifdef MR_DEV_PRIO  // A/B: the wave issuing an event's first loads ahead of the SIMD's other wave
   __builtin_amdgcn_s_setprio(MR_DEV_PRIO);
@@ -1855,7 +1855,7 @@ DI void node_event(const Dev& D, X& x, bool is_msg, uint32_t tnode, uint32_t slo
   if (plo_acc <= phi_acc) pend_note(D, x, me, d, plo_acc, phi_acc, prange_r.x, prange_r.y);
   if constexpr (KV) {
     if (kvready) {
-      kv_flush(D, x, me, d);
+      kv_flush(D, x, me, d, kvready);
       if (x.code != RUN) return;
     }
   }
@@ -2430,11 +2430,17 @@ __global__ void __launch_bounds__(256) reset_kernel(Dev D) {
   CS(CS_CWAKE) = INF_T;
   for (uint32_t q = 0; q < TF_Q; q++) D.tfr[(size_t)x.c * TF_Q + q] = make_uint4(0u, 0u, 0u, 0u);
   if (D.kt32) {  // spawned threads: slot 0 = the test body (+ ck, clerk 0); others empty
-    for (uint32_t s = 0; s < D.nthr; s++) {
+    for (uint32_t s = 0; s < D.nthr; s++)
       for (uint32_t f = 0; f < KT__N; f++) KT(f, s) = 0u;
-      KT(KT_WAKE, s) = INF_T;
-    }
     KT(KT_LIVE, 0) = 1u;
+    // the scheduler keys: empty slots (INF_T, tid 0); slot 0 (the test body: x.twake) and the
+    // pad slot ~0, below no key
+    uint32_t* kw = D.kwk + (size_t)x.c * kws(D.nthr) * 2u;
+    for (uint32_t s = 0; s < kws(D.nthr); s++) {
+      const bool none = s == 0 || s >= D.nthr;
+      kw[2 * s] = none ? ~0u : 0u;
+      kw[2 * s + 1] = none ? ~0u : INF_T;
+    }
   }
   if (D.cfg32)  // shard_ctrler: every server starts with config 0 (num 0, no groups)
     for (uint32_t d = 0; d < D.n; d++) {
