@@ -141,7 +141,7 @@ extern __shared__ uint64_t s_keys_raw[];
 enum : uint32_t {
   P_TAIL, P_SEL, P_DECODE, P_LOAD, P_DROP, P_RVREQ, P_RVREP, P_AEREQ, P_AEREP, P_ISREQ, P_ISREP,
   P_HB, P_ELECT, P_APPLY, P_SEND, P_STORE, P_TESTER, P_STEPDOWN, P_PRO, P_EPI,
-  P_S_SETUP, P_S_NET, P_S_PAY, P_AE_PROBE, P_AP_LOAD, P_AP_CHECK, P__N
+  P_S_SETUP, P_S_NET, P_S_PAY, P_AE_PROBE, P_AP_LOAD, P_AP_CHECK, P_AP_KV, P_AP_PEND, P__N
 };
 #ifdef MR_PROF
 __shared__ unsigned long long s_prof[STEP_BLOCK / 64][2 * P__N + 1];
@@ -461,6 +461,9 @@ DI void reset_timer(const Dev& D, X& x, uint32_t d, NC& n) {  // raft.rs:260-263
 #ifndef MR_RESCAN_OCC  // scan only the occupied slots (A/B: DESIGN.md §6)
 #define MR_RESCAN_OCC 1
 #endif
+#ifndef MR_RESCAN_X4  // A/B: four occupied slots per trip, their LDS reads issued together
+#define MR_RESCAN_X4 0
+#endif
 DI void rescan_min(const Dev& D, X& x) {
   if constexpr (MR_KEY32) {
     uint32_t bt = ~0u, bk = ~0u, bs = 0;
@@ -469,6 +472,28 @@ DI void rescan_min(const Dev& D, X& x) {
     for (uint32_t w = 0; w < MW; w++) {
       const uint32_t mw = D.M > 64u * w ? D.M - 64u * w : 0u;
       uint64_t occ = ~x.free_mask[w] & (mw >= 64 ? ~0ull : ((1ull << mw) - 1ull));
+      if constexpr (MR_RESCAN_X4) {  // four occupied slots per trip, their LDS reads issued together
+        while (occ) {
+          uint32_t s4[4];
+          bool v4[4];
+#pragma unroll
+          for (uint32_t q = 0; q < 4; q++) {
+            v4[q] = occ != 0ull;
+            s4[q] = v4[q] ? 64u * w + (uint32_t)__builtin_ctzll(occ) : 64u * w;
+            occ &= occ - 1ull;
+          }
+          uint32_t k4[4];
+#pragma unroll
+          for (uint32_t q = 0; q < 4; q++) k4[q] = (uint32_t)LK(s4[q]);
+#pragma unroll
+          for (uint32_t q = 0; q < 4; q++) {
+            if (!v4[q]) continue;
+            const uint32_t t = k4[q] >> 5;
+            tie = t == bt || (tie && t > bt);
+            if (t < bt) { bt = t; bk = k4[q]; bs = s4[q]; }
+          }
+        }
+      }
       while (occ) {
         const uint32_t s = 64u * w + (uint32_t)__builtin_ctzll(occ);
         occ &= occ - 1ull;
@@ -498,9 +523,6 @@ DI void rescan_min(const Dev& D, X& x) {
   }
   uint64_t best = ~0ull;
   uint32_t bs = 0;
-#ifndef MR_RESCAN_X4  // A/B: four occupied slots per trip, their LDS reads issued together
-#define MR_RESCAN_X4 0
-#endif
   if constexpr (MR_RESCAN_X4 && MW == 1) {
     uint64_t occ = ~x.free_mask[0] & (D.M >= 64 ? ~0ull : ((1ull << D.M) - 1ull));
     while (occ) {
@@ -756,6 +778,22 @@ DI void node_apply(const Dev& D, X& x, uint32_t me, NC& d, uint32_t& kvready) {
   uint32_t len = d.slen;
   uint32_t pm = 0;  // KV: the server's occupied pending-request slots (kv_apply)
   if constexpr (KV) pm = KVP(me)[KVR_PMASK];
+#ifndef MR_KV_PIDX  // KV: the pending slots' log indices read once per applier visit (A/B round 4)
+#define MR_KV_PIDX 0
+#endif
+  // each pending slot's log index, loaded with the mask (a freed slot's is 0, never an applied
+  // index; the indices do not change while the applier runs): an entry's answers then load only
+  // the slots waiting for its index, not a round trip per occupied slot
+  uint32_t pidx[KV_PEND];
+#pragma unroll
+  for (uint32_t q = 0; q < KV_PEND; q++) pidx[q] = (KV && MR_KV_PIDX) ? KVP(me)[KVR_PEND + 8u * q] : 0u;
+  auto pwait = [&](uint32_t i) -> uint32_t {  // the occupied slots waiting for index i
+    if (!(KV && MR_KV_PIDX)) return pm;
+    uint32_t mm = 0;
+#pragma unroll
+    for (uint32_t q = 0; q < KV_PEND; q++) mm |= (pidx[q] == i ? 1u : 0u) << q;
+    return pm & mm;
+  };
 #if MR_AP_PIPE
   // software-pipelined: batch b + 1's loads are issued before batch b's checker stores, so
   // they do not wait behind them on vmcnt (disjoint indices: a batch never reads what an
@@ -862,7 +900,7 @@ DI void node_apply(const Dev& D, X& x, uint32_t me, NC& d, uint32_t& kvready) {
           for (uint32_t q = 0; q < j; q++) conf |= pkey[q] == pkey[j] || pcl[q] == pcl[j];
           pre = !conf;
         }
-        kv_apply<is_ctrl(S)>(D, x, me, i, ce[j].val, kvready, pm, pre, pka[j], pkb[j], pdd[j]);
+        kv_apply<is_ctrl(S)>(D, x, me, i, ce[j].val, kvready, pwait(i), pre, pka[j], pkb[j], pdd[j]);
         if (x.code != RUN) return;
       }
       if constexpr (kv_gen(S).maxraft > 0) {  // the KV service snapshots (SEMANTICS §9)
@@ -916,7 +954,7 @@ DI void node_apply(const Dev& D, X& x, uint32_t me, NC& d, uint32_t& kvready) {
         CADD(CNT_SNAPSHOTS, 1u);
       }
       if constexpr (KV) {
-        kv_apply<is_ctrl(S)>(D, x, me, i, e[j].val, kvready, pm);
+        kv_apply<is_ctrl(S)>(D, x, me, i, e[j].val, kvready, pwait(i));
         if (x.code != RUN) return;
       }
       if constexpr (kv_gen(S).maxraft > 0) {  // the KV service snapshots (SEMANTICS §9)
@@ -1488,7 +1526,7 @@ DI void node_event(const Dev& D, X& x, bool is_msg, uint32_t tnode, uint32_t slo
     }
     if constexpr (KV) {
       if (type == M_KV_REQ) {  // no Raft term: handled before the step-down rule
-        kv_request(D, x, me, d, src, inc, mterm, ma, mb, mc);
+        kv_request(D, x, me, d, src, inc, mterm, ma, mb, mc, prange_r);
         if (x.code != RUN) return;
         store_node(D, x, me, d);
         nr_set(D, x, nr, 0, type, me, seq, d);

@@ -12,7 +12,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__)))) 
 
 NAMES = ["tail", "sel", "decode", "load", "drop", "rv_req", "rv_rep", "ae_req", "ae_rep",
          "is_req", "is_rep", "hb", "elect", "apply", "send", "store", "tester", "stepdown",
-         "prologue", "epilogue", "s_setup", "s_net", "s_pay", "ae_probe", "ap_load", "ap_check"]
+         "prologue", "epilogue", "s_setup", "s_net", "s_pay", "ae_probe", "ap_load", "ap_check", "ap_kv", "ap_pend"]
 
 if len(sys.argv) > 1 and sys.argv[1] == "--child":
     import torch  # noqa: F401  (HIP runtime first, as in bench.py)
