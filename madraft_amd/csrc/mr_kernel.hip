@@ -770,8 +770,53 @@ enum : uint32_t { SEND_NONE = 0, SEND_REPLY, SEND_APPEND, SEND_VOTE };
 // (tester.rs:366-396) inlined: committed entries are walked in batches of AC
 // whose loads (log entry, storage mask / value) are all issued before any is
 // used — entries have distinct indices, so a batch never reads what it writes.
+// A copy of the kernel arguments whose fields are each their own scalar value (an opaque `asm`
+// per field, pointers cast back to the global address space so loads stay global_load): the
+// kernel-argument words otherwise live as 16-register tuples (s_load_dwordx16) that, spilled to
+// VGPR lanes, are reloaded whole (16 v_readlane) wherever one of their fields is used. On it:
+// the node event (MR_NE_LAUNDER, headline kernel 1 662 -> 988 v_readlane, VALU -9 %) or, as an
+// A/B, only the applier (MR_AP_LAUNDER). Fields the scenario fixes at compile time are left alone.
+#ifndef MR_AP_LAUNDER
+#define MR_AP_LAUNDER 0
+#endif
+template <class T>
+DI T* glp(T* p) {
+  uint64_t v = (uint64_t)(uintptr_t)p;
+  asm volatile("" : "+s"(v));
+  return (T*)((__attribute__((address_space(1))) T*)(uintptr_t)v);
+}
+DI uint32_t glu(uint32_t v) {
+  asm volatile("" : "+s"(v));
+  return v;
+}
+DI Dev dev_launder(const Dev& D0) {
+  Dev D = D0;
+  D.log = glp(D0.log); D.stor = glp(D0.stor); D.cs32 = glp(D0.cs32); D.nd32 = glp(D0.nd32);
+  if (D0.kv32) D.kv32 = glp(D0.kv32);
+  if (D0.kvs32) D.kvs32 = glp(D0.kvs32);
+  if (D0.kring) D.kring = glp(D0.kring);
+  D.trace = glp(D0.trace);
+  D.apply_cap = glu(D0.apply_cap); D.log_cap = glu(D0.log_cap); D.bugs = glu(D0.bugs);
+  D.trace_clusters = glu(D0.trace_clusters); D.trace_cap = glu(D0.trace_cap);
+#ifndef MR_LAUNDER_ALL  // every field the node event reads, not only the applier's
+#define MR_LAUNDER_ALL 1
+#endif
+  if (MR_LAUNDER_ALL) {
+    D.ms32 = glp(D0.ms32); D.pay = glp(D0.pay); D.tmr = glp(D0.tmr);
+    if (D0.led) D.led = glp(D0.led);
+    if (D0.lin32) D.lin32 = glp(D0.lin32);
+    if (D0.kt32) D.kt32 = glp(D0.kt32);
+    if (D0.kwk) D.kwk = glp(D0.kwk);
+    D.seed0 = ((uint64_t)glu((uint32_t)(D0.seed0 >> 32)) << 32) | glu((uint32_t)D0.seed0);
+    D.M = glu(D0.M); D.K = glu(D0.K); D.hb = glu(D0.hb); D.elo = glu(D0.elo); D.ehi = glu(D0.ehi);
+    D.safety = glu(D0.safety); D.max_events = glu(D0.max_events);
+  }
+  return D;
+}
+
 template <uint32_t S>
-DI void node_apply(const Dev& D, X& x, uint32_t me, NC& d, uint32_t& kvready) {
+DI void node_apply(const Dev& Darg, X& x, uint32_t me, NC& d, uint32_t& kvready) {
+  const Dev D = MR_AP_LAUNDER ? dev_launder(Darg) : Darg;
   constexpr bool KV = is_svc(S);
   const bool snapmode = (x.netmode >> 1) & 1u;
   SE* const sb = D.stor + (size_t)x.c * D.apply_cap;
@@ -998,7 +1043,8 @@ DI void node_apply(const Dev& D, X& x, uint32_t me, NC& d, uint32_t& kvready) {
 #define MR_AP_COOP 1
 #endif
 template <uint32_t S>
-DI void node_apply_coop(const Dev& D, X& x, uint32_t me, NC& d) {
+DI void node_apply_coop(const Dev& Darg, X& x, uint32_t me, NC& d) {
+  const Dev D = MR_AP_LAUNDER ? dev_launder(Darg) : Darg;
   // snap_common (the 2D tests, uses_service_snapshots) runs with service snapshots:
   // t_new(snapshot = true) precedes every node event of such a batch, so the mode is the same
   // for every lane here. A scenario whose runtime mode (x.netmode bit 1, what node_apply
@@ -1376,9 +1422,16 @@ DI bool ae_recv_coop(const Dev& D, X& x, uint32_t me, NC& d, uint32_t src, bool 
   return true;
 }
 
+// the whole node event on the laundered argument copy (dev_launder). Same-box A/B, round 4
+// (profiles/r04_ab_round4.txt ab15): figure_8_unreliable_2c 125.6 -> 121.8 ms, its crash variant
+// 67.2 -> 63.6, C5 183 -> 176, C5-lin 561 -> 528 / 690 -> 675; the tester on it too: worse
+#ifndef MR_NE_LAUNDER
+#define MR_NE_LAUNDER 1
+#endif
 template <uint32_t S>
-DI void node_event(const Dev& D, X& x, bool is_msg, uint32_t tnode, uint32_t slot,
+DI void node_event(const Dev& Darg, X& x, bool is_msg, uint32_t tnode, uint32_t slot,
                    uint32_t seq, NR& nr) {
+  const Dev D = MR_NE_LAUNDER ? dev_launder(Darg) : Darg;
   constexpr bool KV = is_svc(S);  // kvraft / shard_ctrler request path
   uint32_t me = tnode, src = 0, type = 0, inc = 0, k = 0, mterm = 0, ma = 0, mb = 0, mc = 0;
   uint32_t kvready = 0;  // KV: the pending-request slots answered in this event (kv_flush)
@@ -2096,11 +2149,15 @@ DI void t_end(const Dev& D, X& x) {  // tester.rs:339-358
 DI uint32_t nd_role(const Dev& D, X& x, uint32_t i) { return f_role(ND(NF_FLAGS, i)); }
 DI uint32_t nd_term(const Dev& D, X& x, uint32_t i) { return ND(NF_TERM, i); }
 #define TV(k) C64(C64_TV + (k))
+#ifndef MR_T_LAUNDER  // A/B: the tester (body and threads) on the laundered argument copy
+#define MR_T_LAUNDER 0
+#endif
 #include "mr_tester.inc"
 
 // one tester event: resume the cluster's coroutine until it sleeps or ends
 template <uint32_t S>
-DI void tester(const Dev& D, X& x) {
+DI void tester(const Dev& Darg, X& x) {
+  const Dev D = MR_T_LAUNDER ? dev_launder(Darg) : Darg;
   T t;
 #ifdef MR_DEV_PRIO
   __builtin_amdgcn_s_setprio(MR_DEV_PRIO);
