@@ -789,12 +789,16 @@ DI uint32_t glu(uint32_t v) {
   asm volatile("" : "+s"(v));
   return v;
 }
+#ifndef MR_LAUNDER_S  // only the fields scenario S has (its arrays and services), not a runtime test
+#define MR_LAUNDER_S 1
+#endif
+template <uint32_t S>
 DI Dev dev_launder(const Dev& D0) {
   Dev D = D0;
   D.log = glp(D0.log); D.stor = glp(D0.stor); D.cs32 = glp(D0.cs32); D.nd32 = glp(D0.nd32);
-  if (D0.kv32) D.kv32 = glp(D0.kv32);
-  if (D0.kvs32) D.kvs32 = glp(D0.kvs32);
-  if (D0.kring) D.kring = glp(D0.kring);
+  if (MR_LAUNDER_S ? is_svc(S) : D0.kv32 != nullptr) D.kv32 = glp(D0.kv32);
+  if (MR_LAUNDER_S ? kv_gen(S).maxraft > 0 : D0.kvs32 != nullptr) D.kvs32 = glp(D0.kvs32);
+  if (MR_LAUNDER_S ? kv_gen(S).maxraft > 0 : D0.kring != nullptr) D.kring = glp(D0.kring);
   D.trace = glp(D0.trace);
   D.apply_cap = glu(D0.apply_cap); D.log_cap = glu(D0.log_cap); D.bugs = glu(D0.bugs);
   D.trace_clusters = glu(D0.trace_clusters); D.trace_cap = glu(D0.trace_cap);
@@ -804,9 +808,9 @@ DI Dev dev_launder(const Dev& D0) {
   if (MR_LAUNDER_ALL) {
     D.ms32 = glp(D0.ms32); D.pay = glp(D0.pay); D.tmr = glp(D0.tmr);
     if (D0.led) D.led = glp(D0.led);
-    if (D0.lin32) D.lin32 = glp(D0.lin32);
-    if (D0.kt32) D.kt32 = glp(D0.kt32);
-    if (D0.kwk) D.kwk = glp(D0.kwk);
+    if (MR_LAUNDER_S ? is_kv(S) : D0.lin32 != nullptr) D.lin32 = glp(D0.lin32);
+    if (MR_LAUNDER_S ? nthr(S) > 0 : D0.kt32 != nullptr) D.kt32 = glp(D0.kt32);
+    if (MR_LAUNDER_S ? nthr(S) > 0 : D0.kwk != nullptr) D.kwk = glp(D0.kwk);
     D.seed0 = ((uint64_t)glu((uint32_t)(D0.seed0 >> 32)) << 32) | glu((uint32_t)D0.seed0);
     D.M = glu(D0.M); D.K = glu(D0.K); D.hb = glu(D0.hb); D.elo = glu(D0.elo); D.ehi = glu(D0.ehi);
     D.safety = glu(D0.safety); D.max_events = glu(D0.max_events);
@@ -816,7 +820,7 @@ DI Dev dev_launder(const Dev& D0) {
 
 template <uint32_t S>
 DI void node_apply(const Dev& Darg, X& x, uint32_t me, NC& d, uint32_t& kvready) {
-  const Dev D = MR_AP_LAUNDER ? dev_launder(Darg) : Darg;
+  const Dev D = MR_AP_LAUNDER ? dev_launder<S>(Darg) : Darg;
   constexpr bool KV = is_svc(S);
   const bool snapmode = (x.netmode >> 1) & 1u;
   SE* const sb = D.stor + (size_t)x.c * D.apply_cap;
@@ -1044,7 +1048,7 @@ DI void node_apply(const Dev& Darg, X& x, uint32_t me, NC& d, uint32_t& kvready)
 #endif
 template <uint32_t S>
 DI void node_apply_coop(const Dev& Darg, X& x, uint32_t me, NC& d) {
-  const Dev D = MR_AP_LAUNDER ? dev_launder(Darg) : Darg;
+  const Dev D = MR_AP_LAUNDER ? dev_launder<S>(Darg) : Darg;
   // snap_common (the 2D tests, uses_service_snapshots) runs with service snapshots:
   // t_new(snapshot = true) precedes every node event of such a batch, so the mode is the same
   // for every lane here. A scenario whose runtime mode (x.netmode bit 1, what node_apply
@@ -1226,6 +1230,9 @@ DI uint32_t on_ack(const Dev& D, X& x, uint32_t me, NC& d, uint32_t p, uint32_t 
 // AC entries j.. of an AppendEntries payload (the sender's ring, or the
 // materialized copy) and the receiver's entries at their indices: their terms, and (MR_F_SAFETY
 // log matching) their commands, from one 16-B load per entry
+#ifndef MR_AE_PIPE  // A/B: AppendEntries receive batches software-pipelined (node_event)
+#define MR_AE_PIPE 0
+#endif
 #ifndef MR_AE_OWN  // 5-server kernels: yes (+0.7 %); 7 / 8: no (118 -> 4 spilled VGPRs at NB = 7)
 #define MR_AE_OWN (MR_NB <= 5)
 #endif
@@ -1431,7 +1438,7 @@ DI bool ae_recv_coop(const Dev& D, X& x, uint32_t me, NC& d, uint32_t src, bool 
 template <uint32_t S>
 DI void node_event(const Dev& Darg, X& x, bool is_msg, uint32_t tnode, uint32_t slot,
                    uint32_t seq, NR& nr) {
-  const Dev D = MR_NE_LAUNDER ? dev_launder(Darg) : Darg;
+  const Dev D = MR_NE_LAUNDER ? dev_launder<S>(Darg) : Darg;
   constexpr bool KV = is_svc(S);  // kvraft / shard_ctrler request path
   uint32_t me = tnode, src = 0, type = 0, inc = 0, k = 0, mterm = 0, ma = 0, mb = 0, mc = 0;
   uint32_t kvready = 0;  // KV: the pending-request slots answered in this event (kv_flush)
@@ -1692,7 +1699,7 @@ DI void node_event(const Dev& Darg, X& x, bool is_msg, uint32_t tnode, uint32_t 
 #else
         for (uint32_t j = j0; j < jw; j += AC) {
 #endif
-          if (j != j0) ae_load_batch(D, x, me, d, src, mat, pp, ma, k, j, pe, lt, ov, ors);
+          if (!MR_AE_PIPE && j != j0) ae_load_batch(D, x, me, d, src, mat, pp, ma, k, j, pe, lt, ov, ors);
           if (D.safety) {  // MR_F_SAFETY log matching: same index and term => same entry
 #if !MR_AE_OWN
 #pragma unroll
@@ -1708,6 +1715,14 @@ DI void node_event(const Dev& Darg, X& x, bool is_msg, uint32_t tnode, uint32_t 
             }
             if (bad) { fail(D, x, MR_FAIL_SAFETY_LOG_MATCHING); return; }
           }
+          // MR_AE_PIPE: the next batch's loads issued before this batch's log writes, so they do
+          // not wait behind those stores (vmcnt retires in issue order). Safe: the next batch's
+          // indices are other ring slots, and its own-entry terms are only trusted below the
+          // current last (the skip test re-reads d.last, which a write can only lower to its index)
+          LE pe2[AC];
+          uint32_t lt2[AC], ors2[AC];
+          uint64_t ov2[AC];
+          if (MR_AE_PIPE && j + AC < jw) ae_load_batch(D, x, me, d, src, mat, pp, ma, k, j + AC, pe2, lt2, ov2, ors2);
 #pragma unroll
           for (uint32_t q = 0; q < AC; q++) {
             const uint32_t jx = j + q, i = ma + 1 + jx;
@@ -1731,6 +1746,10 @@ DI void node_event(const Dev& Darg, X& x, bool is_msg, uint32_t tnode, uint32_t 
             d.last = i;
             d.lastt = pe[q].term;
             CMAX(CNT_MAX_LOG, i - d.snap);
+          }
+          if (MR_AE_PIPE && j + AC < jw) {
+#pragma unroll
+            for (uint32_t q = 0; q < AC; q++) { pe[q] = pe2[q]; lt[q] = lt2[q]; ov[q] = ov2[q]; ors[q] = ors2[q]; }
           }
         }
 #ifdef MR_DEV_AEDBG
@@ -2157,7 +2176,7 @@ DI uint32_t nd_term(const Dev& D, X& x, uint32_t i) { return ND(NF_TERM, i); }
 // one tester event: resume the cluster's coroutine until it sleeps or ends
 template <uint32_t S>
 DI void tester(const Dev& Darg, X& x) {
-  const Dev D = MR_T_LAUNDER ? dev_launder(Darg) : Darg;
+  const Dev D = MR_T_LAUNDER ? dev_launder<S>(Darg) : Darg;
   T t;
 #ifdef MR_DEV_PRIO
   __builtin_amdgcn_s_setprio(MR_DEV_PRIO);
