@@ -461,8 +461,11 @@ DI void reset_timer(const Dev& D, X& x, uint32_t d, NC& n) {  // raft.rs:260-263
 #ifndef MR_RESCAN_OCC  // scan only the occupied slots (A/B: DESIGN.md §6)
 #define MR_RESCAN_OCC 1
 #endif
-#ifndef MR_RESCAN_X4  // A/B: four occupied slots per trip, their LDS reads issued together
-#define MR_RESCAN_X4 0
+// the earliest-message rescan four occupied slots per trip, their LDS reads issued together:
+// after the argument laundering (ab20) figure_8_unreliable_2c +1.2 %, crash +0.6 %, C5 +1 %
+// (ab11), the 3-server 2D kernel −1.3 % (ab20): on for 64-bit keys (the 3- / 5-server kernels)
+#ifndef MR_RESCAN_X4
+#define MR_RESCAN_X4 (!MR_KEY32)
 #endif
 DI void rescan_min(const Dev& D, X& x) {
   if constexpr (MR_KEY32) {
@@ -1288,9 +1291,11 @@ DI void ae_load_batch(const Dev& D, const X& x, uint32_t me, const NC& d, uint32
 // Measured (round 4, same box, profiles/r04_ab_ae_coop.txt): figure_8_unreliable_2c 124.4 -> 125.8 ms,
 // its crash variant -1 %, the 15-clerk linearizable kvraft config +1.4 %; ae_req ticks per visit
 // 570 -> 675 in the section profile (the owner walk's readlanes and the LDS exchange cost more
-// than the batches they replace). Off; kept for the record and for A/B.
+// than the batches they replace). Re-measured after the argument laundering (ab20): 5-server
+// kernels −0.2 / −0.8 %, the 3-server 2D kernel +2.2 %; the 15-clerk kvraft kernels +1.5 / +0.3 %
+// (ab21): on where keys are 32-bit (the 7- / 8-server kernels).
 #ifndef MR_AE_COOP
-#define MR_AE_COOP 0
+#define MR_AE_COOP MR_KEY32
 #endif
 constexpr uint32_t AE_COOP_REM = 12;  // entries after the first batch an owner may hand out (LDS rows)
 DI void wave_sync_lds() {
