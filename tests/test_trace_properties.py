@@ -119,6 +119,7 @@ def test_gpu_traces_hold_raft_properties(hip, test, kw):
     ("figure_8_unreliable_2c", 131072, dict(safety=True)),     # config 3, one GPU's shard
     ("figure_8_unreliable_crash", 131072, dict(safety=True)),  # ... crash-restart + persister
     ("snapshot_install_unreliable_2d", 262144, dict(nodes=7)),  # config 4
+    ("unreliable_3a", 65536, {}),                                # config 5: kvraft servers
 ])
 def test_gpu_traces_at_baseline_size(hip, test, clusters, kw):
     """The same properties on traces taken from a BASELINE-size run: 48 clusters spread over
