@@ -43,6 +43,15 @@ def has_exact(i, nb):
     return nb < 8 and (DEFAULT_N[i] == nb or (i == 5 and nb == 5) or (i in NB7_SCNS and nb == 7))
 
 
+# Raft-only test bodies without spawned threads (mr_dev.h has_pool): the pool-kernel instances
+POOL_SCNS = set(range(1, 15)) | {16} | set(range(19, 25))
+
+
+def has_pool(i, nb):
+    """mr_dev.h has_pool: a pool-kernel instance of scenario i at nb servers is built."""
+    return nb <= 5 and has_exact(i, nb) and i in POOL_SCNS
+
+
 def _units(csrc, scns=None):
     kern = os.path.join(csrc, "mr_kernel.hip")
     units = [(kern, "common", ["-DMR_COMMON=1", "-DMR_SCN_LIST=", "-DMR_NB=8"])]
@@ -63,6 +72,13 @@ def _units(csrc, scns=None):
         for i in wide:  # 256 message slots (mr_kernel.hip MR_MW)
             units.append((kern, f"nb{nb}_w{i}", ["-DMR_COMMON=0", f"-DMR_SCN_LIST=MR_INST({i})",
                                                  f"-DMR_NB={nb}", "-DMR_MW=4", *key]))
+    for nb in (3, 5):  # pool kernels: 32-bit keys
+        ids = [i for i in (scns or SCN_IDS) if has_pool(i, nb)]
+        ng = max(1, min(N_GROUPS, (len(ids) + 2) // 3)) if ids else 0
+        for g in range(ng):
+            lst = " ".join(f"MR_INST({i})" for i in ids[g::ng])
+            units.append((kern, f"pool{nb}_{g}", ["-DMR_COMMON=0", f"-DMR_SCN_LIST={lst}",
+                                                  f"-DMR_NB={nb}", "-DMR_KEY32=1", "-DMR_POOL=1"]))
     ids = list(scns or SCN_IDS)  # decision-tape builds (SEMANTICS §12), NB = 8
     wide = [i for i in ids if i in WIDE_SLOTS]
     ids = [i for i in ids if i not in WIDE_SLOTS]

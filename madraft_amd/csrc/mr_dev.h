@@ -220,6 +220,7 @@ struct Dev {
   unsigned long long* prof;  // [PROF_SLOTS] wave-cycle profile (MR_PROF builds only)
   uint4* tfr;       // [C][TF_Q] the tester coroutine frame, one cluster-major 80-B record
   uint32_t* kwk;    // [C][kws(nthr)][2] thread slots' {tid, wake}: the scheduler's keys, packed
+  uint32_t pool;    // the batch runs on pool_kernel (has_pool): 32-bit keys with the AE bit
 };
 // words-pairs per cluster of kwk: the thread slots rounded up to whole 16-B quads (two slots each;
 // slot 0 = the test body and the pad slot hold ~0, so they never win a rescan)
@@ -286,6 +287,11 @@ constexpr uint32_t nthr(uint32_t s) {
 // sized for its default server count (nb_of) and one for up to 8 servers
 template <uint32_t S, uint32_t NB>
 hipError_t launch_step_t(const Dev& D, uint32_t budget, hipStream_t s);
+// the pool kernel of scenario S (has_pool(S, NB); mr_kernel.hip MR_POOL units)
+template <uint32_t S, uint32_t NB>
+hipError_t launch_pool_t(const Dev& D, uint32_t budget, hipStream_t s);
+template <uint32_t S, uint32_t NB>
+uint32_t pool_capacity_t(int device, uint32_t M);
 // lanes the step kernel of scenario S keeps resident on the device (occupancy x CUs x block)
 template <uint32_t S, uint32_t NB>
 uint32_t step_capacity_t(int device, uint32_t M);
@@ -311,6 +317,13 @@ constexpr bool has_exact(uint32_t s, uint32_t n) {
   return n < 8u && (n == k_default_n[s] || (s == MR_SCN_FAIL_AGREE_2B && n == 5u) ||
                     (has_nb7(s) && n == 7u));
 }
+// pool-kernel instances (mr_kernel.hip pool_kernel): Raft-only test bodies
+// without spawned threads, at an exact server count of 3 or 5 (up to 32 message slots: the
+// 32-bit keys of a 512-cluster pool take 64 KiB of LDS)
+constexpr bool has_pool(uint32_t s, uint32_t n) {
+  return n <= 5u && has_exact(s, n) && !is_svc(s) && nthr(s) == 0;
+}
+constexpr uint32_t POOL_MAX_SLOTS = 32;
 // scenarios whose test body starts the tester with service snapshots (t_new(snapshot = true),
 // tester.rs:303-325 SNAPSHOT_INTERVAL): snap_common's five 2D tests. node_apply_coop specializes
 // on it at compile time and checks it against the runtime mode (x.netmode bit 1).

@@ -21,6 +21,11 @@ namespace mr {
 template <uint32_t S>
 static hipError_t launch_any(const Dev& D, uint32_t budget, hipStream_t s) {
   if (D.tape_mode) return launch_step_tape_t<S, MR_MAX_NODES>(D, budget, s);
+  if (D.pool) {  // the pool kernel (mr_dev.h has_pool; the host sets D.pool only where it exists)
+    if constexpr (has_pool(S, 3)) if (D.n == 3) return launch_pool_t<S, 3>(D, budget, s);
+    if constexpr (has_pool(S, 5)) if (D.n == 5) return launch_pool_t<S, 5>(D, budget, s);
+    return hipErrorInvalidValue;
+  }
   if constexpr (has_exact(S, 3)) if (D.n == 3) return launch_step_t<S, 3>(D, budget, s);
   if constexpr (has_exact(S, 5)) if (D.n == 5) return launch_step_t<S, 5>(D, budget, s);
   if constexpr (has_exact(S, 7)) if (D.n == 7) return launch_step_t<S, 7>(D, budget, s);
@@ -28,6 +33,11 @@ static hipError_t launch_any(const Dev& D, uint32_t budget, hipStream_t s) {
 }
 template <uint32_t S>
 static uint32_t capacity_any(const Dev& D, int device) {
+  if (D.pool) {
+    if constexpr (has_pool(S, 3)) if (D.n == 3) return pool_capacity_t<S, 3>(device, D.M);
+    if constexpr (has_pool(S, 5)) if (D.n == 5) return pool_capacity_t<S, 5>(device, D.M);
+    return 0;
+  }
   if constexpr (has_exact(S, 3)) if (D.n == 3) return step_capacity_t<S, 3>(device, D.M);
   if constexpr (has_exact(S, 5)) if (D.n == 5) return step_capacity_t<S, 5>(device, D.M);
   if constexpr (has_exact(S, 7)) if (D.n == 7) return step_capacity_t<S, 7>(device, D.M);
@@ -59,6 +69,23 @@ static uint32_t step_capacity(const Dev& D, uint32_t scn, int device) {
 #endif
 #undef MR_INST
     default: return 0;
+  }
+}
+// the pool kernel serves this batch: an instance exists, the key rows fit (M <= 32), and the
+// environment does not turn it off (MR_POOL=0: the per-lane step kernel, for A/B runs)
+static bool use_pool(uint32_t scn, uint32_t n, uint32_t M) {
+  if (M > POOL_MAX_SLOTS) return false;
+  if (const char* e = std::getenv("MR_POOL")) if (e[0] == '0') return false;
+  switch (scn) {
+#define MR_INST(S) \
+  case S: return has_pool(S, n);
+#ifdef MR_DEV_SCNS
+    MR_DEV_SCNS
+#else
+    MR_ALL_SCNS
+#endif
+#undef MR_INST
+    default: return false;
   }
 }
 hipError_t launch_reset(const Dev& D, hipStream_t s);
@@ -126,6 +153,7 @@ struct mr_batch {
   uint4* tape = nullptr;     // keyed decisions (own allocation: set_decisions / MR_F_RECORD)
   uint32_t* doff = nullptr;  // replay: CSR row offsets of `tape` (set_decisions)
   bool submitted = false;    // mr_batch_submit enqueued a step not yet finished
+  uint32_t kern = 0;         // kernel family of the launches since the reset: 1 pool, 2 step / tape
   std::chrono::steady_clock::time_point t_submit;
 };
 
@@ -292,6 +320,7 @@ static int mr_batch_create_impl(const mr_cfg* cfg, mr_batch** out) {
                        scn <= MR_SCN_SNAPSHOT_INSTALL_UNRELIABLE_CRASH_2D) ? 30 : 1000;
   D.iters = cfg->iters ? cfg->iters : def_iters;
   D.seed0 = cfg->seed_base + cfg->cluster_base;
+  D.pool = !(cfg->flags & MR_F_RECORD) && use_pool(scn, (uint32_t)n, (uint32_t)M) ? 1u : 0u;
 
   // carve one allocation; every array 256-B aligned
   struct Item { void** p; size_t bytes; };
@@ -405,6 +434,7 @@ static int mr_batch_create_impl(const mr_cfg* cfg, mr_batch** out) {
 
 static int enqueue_reset(mr_batch* b, uint64_t seed_base) {
   b->cfg.seed_base = seed_base;
+  b->kern = 0;
   b->c_open = 0;
   b->resume = false;
   b->D.seed0 = seed_base + b->cfg.cluster_base;
@@ -428,6 +458,12 @@ static int enqueue_reset(mr_batch* b, uint64_t seed_base) {
 // one step-kernel launch on the batch stream, bracketed by the timing events;
 // the remaining-cluster count is copied back asynchronously
 static int enqueue_step(mr_batch* b, uint32_t budget) {
+  // the pool kernel's message keys (32-bit, AppendEntries bit) and the step / tape kernels' are
+  // different HBM formats: a run does not switch family between its launches
+  const uint32_t kern = b->D.pool && !b->D.tape_mode ? 1u : 2u;
+  if (b->kern && b->kern != kern)
+    return set_err("decisions set or dropped in the middle of a pool-kernel run: mr_batch_reset first");
+  b->kern = kern;
   b->h_ctl0[0] = 0;
   if (b->D.stream && b->resume) {  // continue: the held clusters first, the claim pointer kept
     b->h_ctl0[1] = b->h_remaining[1];

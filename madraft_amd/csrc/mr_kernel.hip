@@ -67,8 +67,9 @@ struct X {
   uint64_t free_mask[MW], digest, mmin;
   uint32_t timer[NB];  // node timers (election / heartbeat deadline), INF_T = none
 #if !MR_CNT_MEM
-  uint32_t cnt[CNT__N];
+  uint32_t cnt[CNT__N];  // pool_kernel: the lane's sums over its events (per cluster: POOL_CNT)
 #endif
+  uint32_t ls;  // pool_kernel: the cluster's pool slot (its LDS column)
 };
 
 // field accessors (32-bit element offsets, checked at batch creation)
@@ -124,16 +125,37 @@ static_assert(STEP_BLOCK == 64, "step_kernel's lane mapping assumes one 64-lane 
 #ifndef MR_HB_CLASS  // leaders' heartbeat timers as a sub-class of their own (same rule)
 #define MR_HB_CLASS 0
 #endif
+// MR_POOL: the cluster-pool kernel (pool_kernel below): a workgroup of
+// POOL_WAVES waves shares a pool of POOL_SLOTS clusters whose run state lives in LDS; a wave
+// takes up to 64 ready clusters whose next event is of one kind (the bins). Its translation
+// units use 32-bit keys.
+#ifndef MR_POOL
+#define MR_POOL 0
+#endif
+static_assert(!MR_POOL || MR_KEY32, "the pool kernel keeps 32-bit message keys");
+constexpr uint32_t POOL_WAVES = 8, POOL_SLOTS = 64 * POOL_WAVES;
 using lkey_t = std::conditional_t<MR_KEY32 != 0, uint32_t, uint64_t>;
 constexpr lkey_t LKEY_FREE = ~lkey_t(0);
 constexpr uint32_t T_KEY_MAX = (1u << 27) - 1u;  // delivery times at or past it: SIM_CAPACITY
 extern __shared__ uint64_t s_keys_raw[];
 #define s_keys reinterpret_cast<lkey_t*>(s_keys_raw)
-#define LK(s) s_keys[(s) * STEP_BLOCK + threadIdx.x]
-// send-loop staging after the M keys: next[p] and term at next[p] - 1 (u32)
-#define LNX(p) reinterpret_cast<uint32_t*>(s_keys + D.M * STEP_BLOCK)[(p) * STEP_BLOCK + threadIdx.x]
-#define LPT(p) \
-  reinterpret_cast<uint32_t*>(s_keys + D.M * STEP_BLOCK)[(MR_MAX_NODES + (p)) * STEP_BLOCK + threadIdx.x]
+// key rows: one column per lane (step_kernel) or per pool slot (pool_kernel, x.ls)
+constexpr uint32_t KSTR = MR_POOL ? POOL_SLOTS : STEP_BLOCK;
+#if MR_POOL
+#define LK(s) s_keys[(s) * KSTR + x.ls]
+#else
+#define LK(s) s_keys[(s) * KSTR + threadIdx.x]
+#endif
+// per-wave staging after the M key rows: 16 rows of 64 lanes (u32) for each wave of the block —
+// the send loop's next[p] / term at next[p] - 1, the appliers' and the AppendEntries receive's
+// exchange words
+constexpr uint32_t WSTG_ROWS = 2 * MR_MAX_NODES;
+DI uint32_t* wstg(const Dev& D) {
+  return reinterpret_cast<uint32_t*>(s_keys + D.M * KSTR) + (threadIdx.x >> 6) * (WSTG_ROWS * 64u);
+}
+DI uint32_t lane64() { return threadIdx.x & 63u; }
+#define LNX(p) wstg(D)[(p) * 64u + lane64()]
+#define LPT(p) wstg(D)[(MR_MAX_NODES + (p)) * 64u + lane64()]
 
 // Development profile (MR_PROF builds): the first active lane of a wave adds
 // the wave cycles since the previous mark to section k, so the sections
@@ -144,7 +166,7 @@ enum : uint32_t {
   P_S_SETUP, P_S_NET, P_S_PAY, P_AE_PROBE, P_AP_LOAD, P_AP_CHECK, P_AP_KV, P_AP_PEND, P__N
 };
 #ifdef MR_PROF
-__shared__ unsigned long long s_prof[STEP_BLOCK / 64][2 * P__N + 1];
+__shared__ unsigned long long s_prof[MR_POOL ? POOL_WAVES : 1][2 * P__N + 1];
 #define PROF(k)                                                            \
   do {                                                                     \
     unsigned long long t_ = wall_clock64();                                \
@@ -631,9 +653,12 @@ DI int net_send(const Dev& D, X& x, uint32_t src, uint32_t& nctr, uint32_t dst, 
   x.inflight++;
   CMAX(CNT_MAX_INFLIGHT, x.inflight);
   if constexpr (MR_KEY32) {
-    LK(slot) = (t << 5) | dst;
+    // pool kernels (Raft-only, dst < 8): bit 3 marks an AppendEntries request, the event kind
+    // the pool bins by (pool_kind); dst is key & 7 there
+    const uint32_t lo = MR_POOL && type == M_AE_REQ ? dst | 8u : dst;
+    LK(slot) = (t << 5) | lo;
     // every message in flight has a smaller seq: a new one is earliest only by time
-    if (t < (uint32_t)(x.mmin >> 32)) { x.mmin = ((uint64_t)t << 32) | dst; x.mslot = slot; }
+    if (t < (uint32_t)(x.mmin >> 32)) { x.mmin = ((uint64_t)t << 32) | lo; x.mslot = slot; }
   } else {
     // bit 5: AppendEntries request (the step loop's AE sub-class, MR_AE_CLASS); below the
     // unique seq, so it never decides the order
@@ -1062,10 +1087,10 @@ DI void node_apply_coop(const Dev& Darg, X& x, uint32_t me, NC& d) {
   const uint32_t base = d.applied + 1u, len0 = d.slen;
   // per-owner LDS words (the send-loop staging, unused until the send loop): first failure
   // key, last snapshot's term
-  uint32_t* const fkw = reinterpret_cast<uint32_t*>(s_keys + D.M * STEP_BLOCK);
-  uint32_t* const stw = fkw + STEP_BLOCK;
-  const uint32_t lane = __lane_id(), wave0 = threadIdx.x - lane;
-  if (cnt) fkw[threadIdx.x] = ~0u;
+  uint32_t* const fkw = wstg(D);
+  uint32_t* const stw = fkw + 64u;
+  const uint32_t lane = lane64();
+  if (cnt) fkw[lane] = ~0u;
   const uint64_t act = __ballot(1);
   const uint64_t own = __ballot(cnt != 0u);
   const uint32_t nh = (uint32_t)__popcll(act);
@@ -1120,13 +1145,13 @@ DI void node_apply_coop(const Dev& Darg, X& x, uint32_t me, NC& d) {
     if (__ballot(key != ~0u)) anyfail = true;
     if (anyfail) {
       if (key != ~0u)
-        __hip_atomic_fetch_min(&fkw[wave0 + o], key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+        __hip_atomic_fetch_min(&fkw[o], key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
       __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
       __builtin_amdgcn_wave_barrier();
     }
     // phase 2: entries below the owner's first failure are applied
     if (mine) {
-      const uint32_t fk = anyfail ? fkw[wave0 + o] : ~0u;
+      const uint32_t fk = anyfail ? fkw[o] : ~0u;
       const uint32_t f = fk == ~0u ? ~0u : fk >> 2;
       if (i < f && i >= olen)  // i == len in node_apply's walk: appended
         D.stor[(size_t)oc * D.apply_cap + i] = SE{e.val, s.mask | (1u << ome), e.term};
@@ -1134,7 +1159,7 @@ DI void node_apply_coop(const Dev& Darg, X& x, uint32_t me, NC& d) {
         // the last snapshot index of the applied range [obase, min(oend, f - 1)]
         const uint32_t hi = f <= oend ? f - 1u : oend;
         if (hi - i < 10u) {  // no later one in range: this entry is the snapshot kept
-          stw[wave0 + o] = e.term;
+          stw[o] = e.term;
           *reinterpret_cast<uint64_t*>(D.nd32 + ((size_t)oc * D.n + ome) * NREC + NF_SNAPV) = e.val;
         }
       }
@@ -1146,7 +1171,7 @@ DI void node_apply_coop(const Dev& Darg, X& x, uint32_t me, NC& d) {
   }
   if (!cnt) return;
   // the owner: counters and node state as node_apply leaves them
-  const uint32_t fk = anyfail ? fkw[threadIdx.x] : ~0u;
+  const uint32_t fk = anyfail ? fkw[lane] : ~0u;
   const uint32_t end = fk == ~0u ? d.commit : (fk >> 2) - 1u;  // last entry applied in full
   const uint32_t napplied = end + 1u - base;                    // may be 0 (f == base)
   CADD(CNT_APPLIES, napplied + (fk != ~0u && (fk & 3u) != 0u ? 1u : 0u));
@@ -1160,7 +1185,7 @@ DI void node_apply_coop(const Dev& Darg, X& x, uint32_t me, NC& d) {
     if (first <= end) {
       const uint32_t k = (end - first) / 10u + 1u;
       d.snap = first + 10u * (k - 1u);
-      d.snapt = stw[threadIdx.x];
+      d.snapt = stw[lane];
       CADD(CNT_SNAPSHOTS, k);
     }
   }
@@ -1309,12 +1334,12 @@ DI uint32_t rl(uint32_t v, uint32_t lane) {
 DI bool ae_recv_coop(const Dev& D, X& x, uint32_t me, NC& d, uint32_t src, bool mat, uint32_t slot,
                      uint32_t ma, uint32_t k, uint32_t jr, uint32_t lrs, uint32_t& tprev,
                      uint32_t& rsprev, bool& wrote, uint32_t plo, uint32_t phi) {
-  uint32_t* const stg = reinterpret_cast<uint32_t*>(s_keys + D.M * STEP_BLOCK);
+  uint32_t* const stg = wstg(D);
   uint32_t* const fw = stg;                    // row 0: first entry written (j), per owner
-  uint32_t* const bw = stg + STEP_BLOCK;       // row 1: first skipped entry with another command
-  uint32_t* const mw = stg + 4 * STEP_BLOCK;   // rows 4..15: our rs at jr + r (matched entries);
+  uint32_t* const bw = stg + 64u;              // row 1: first skipped entry with another command
+  uint32_t* const mw = stg + 4u * 64u;         // rows 4..15: our rs at jr + r (matched entries);
                                                // pass 2: rows 4 / 5 = rs / term of the last written
-  const uint32_t lane = threadIdx.x;           // one wave per block (static_assert STEP_BLOCK)
+  const uint32_t lane = lane64();
   const uint32_t cnt = k > jr ? k - jr : 0u;
   // entries from jp on are past our log (index ma + 1 + j > last): never a match
   const uint32_t jp = d.last - ma;  // prev <= last and ma <= prev (a snapshot skip raises prev)
@@ -1360,7 +1385,7 @@ DI bool ae_recv_coop(const Dev& D, X& x, uint32_t me, NC& d, uint32_t src, bool 
         if (ot != pe.term) {
           __hip_atomic_fetch_min(&fw[o], j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
         } else {
-          mw[jx * STEP_BLOCK + o] = ors;
+          mw[jx * 64u + o] = ors;
           if (D.safety && ow.val != pe.val)
             __hip_atomic_fetch_min(&bw[o], j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
         }
@@ -1381,7 +1406,7 @@ DI bool ae_recv_coop(const Dev& D, X& x, uint32_t me, NC& d, uint32_t src, bool 
     } else {
       jend = f;
     }
-    rsf = f == jr ? rsprev : mw[(f - 1u - jr) * STEP_BLOCK + lane];
+    rsf = f == jr ? rsprev : mw[(f - 1u - jr) * 64u + lane];
     if (jend > f && x.now <= d.pexp && plo <= phi) {  // guard_log_write over [index(f), index(jend - 1)]
       const uint32_t a = ma + 1u + f, len = jend - 1u - f, span = phi - plo;
       const uint32_t u = (a - plo) & (D.log_cap - 1u);
@@ -1417,7 +1442,7 @@ DI bool ae_recv_coop(const Dev& D, X& x, uint32_t me, NC& d, uint32_t src, bool 
                                  : D.log[((size_t)oc * D.n + osrc) * D.log_cap + ri];
         const uint32_t rs = pe.rs >= oma + 1u + of ? pe.rs : orsf;
         D.log[((size_t)oc * D.n + ome) * D.log_cap + ri] = LE{pe.term, rs, pe.val};
-        if (j + 1u == (ofe >> 8)) { mw[o] = rs; mw[STEP_BLOCK + o] = pe.term; }
+        if (j + 1u == (ofe >> 8)) { mw[o] = rs; mw[64u + o] = pe.term; }
       }
     }
     wave_sync_lds();
@@ -1426,7 +1451,7 @@ DI bool ae_recv_coop(const Dev& D, X& x, uint32_t me, NC& d, uint32_t src, bool 
     wrote = true;
     d.last = ma + jend;
     rsprev = mw[lane];
-    tprev = d.lastt = mw[STEP_BLOCK + lane];
+    tprev = d.lastt = mw[64u + lane];
     CADD(CNT_LOG_WRITES, c2);
     CMAX(CNT_MAX_LOG, d.last - d.snap);
   }
@@ -2517,6 +2542,10 @@ __global__ void __launch_bounds__(STEP_BLOCK, step_waves<S>()) step_kernel(Dev D
   }
 }
 
+#if MR_POOL
+#include "mr_pool.inc"
+#endif
+
 #ifndef MR_COMMON
 #define MR_COMMON 1
 #endif
@@ -2651,6 +2680,10 @@ uint32_t step_capacity_t(int device, uint32_t M) {
 #endif
 #if MR_TAPE  // replay / record batches run one launch of all their clusters
 #define MR_INST(S) template hipError_t launch_step_t<S, MR_NB>(const Dev&, uint32_t, hipStream_t);
+#elif MR_POOL
+#define MR_INST(S)                                                                     \
+  template hipError_t launch_pool_t<S, MR_NB>(const Dev&, uint32_t, hipStream_t);      \
+  template uint32_t pool_capacity_t<S, MR_NB>(int, uint32_t);
 #else
 #define MR_INST(S)                                                                     \
   template hipError_t launch_step_t<S, MR_NB>(const Dev&, uint32_t, hipStream_t);      \
