@@ -44,7 +44,7 @@ constexpr uint32_t T_NV = 16;  // u64 script arrays (count_2b / concurrent_start
 // cs32 [CS__N][C]: per-cluster u32 scalars
 enum : uint32_t {
   CS_CODE, CS_VTIME, CS_NOW, CS_EVENTS, CS_MSGS, CS_INFLIGHT, CS_NETMODE, CS_TCTR, CS_TRACEN,
-  CS_MSLOT, CS_CONN, CS_ALIVE, CS_TPC, CS_TWAKE, CS_TRES, CS_TL, CS_TH = CS_TL + T_NL, CS_CNT = CS_TH + T_NH,
+  CS_MSLOT, CS_CONN, CS_ALIVE, CS_TWAKE, CS_CNT,  // (the tester frame is the tfr record)
   CS_KVDONE = CS_CNT + CNT__N, CS_MJOIN, CS_CWAKE, CS_CTID, CS_CSLOT,  // tester threads (SEMANTICS §8-9)
   CS_NLIVE,  // live spawned threads
   CS_NOPS,   // shard_ctrler: clerk operations so far
@@ -62,11 +62,12 @@ enum : uint32_t {
 };
 // cs64 [C64__N][C]: per-cluster u64 scalars
 // C64_FREE1..3: free-slot mask words 1..3 (slots 64..255, MR_MW = 4 units)
-enum : uint32_t { C64_FREE, C64_DIGEST, C64_MMIN, C64_THV, C64_TV, C64_FREE1 = C64_TV + T_NV,
+enum : uint32_t { C64_FREE, C64_DIGEST, C64_MMIN, C64_TV, C64_FREE1 = C64_TV + T_NV,
                   C64__N = C64_FREE1 + 3 };
-// Cluster scalars: cluster-major records (MR_CS_MAJOR, default) — cs32[c][CS_STRIDE],
-// cs64[c][C64_STRIDE] — so a kernel reaches any field from one per-lane base plus a constant
-// offset; or cluster-minor matrices [field][C]. The host reads rows through these index macros.
+// Cluster scalars: cluster-minor matrices [field][C] (the default: a wave's lanes read 64
+// consecutive words of one field), or, with MR_CS_MAJOR=1 (an A/B option, measured -5 %),
+// cluster-major records cs32[c][CS_STRIDE] / cs64[c][C64_STRIDE]. The host reads rows through
+// these index macros.
 #ifndef MR_CS_MAJOR
 #define MR_CS_MAJOR 0
 #endif
@@ -111,7 +112,7 @@ constexpr uint32_t KV_PEND = 8;     // pending requests per server
 // Words KT_W.. are the thread's own frame: kvraft clerk fields, churn client
 // (x lo/hi, index, timeout step, values), or a one() task (helper frame h[0..4], cmd).
 enum : uint32_t {
-  KT_TID, KT_LIVE, KT_PC, KT_J, KT_CLI, KT_TCTR, KT_WAKE /* unused: kwk */, KT_ID, KT_LH, KT_SEQ, KT_TAG, KT_NCTR,
+  KT_TID, KT_LIVE, KT_PC, KT_J, KT_CLI, KT_TCTR, KT_ID, KT_LH, KT_SEQ, KT_TAG, KT_NCTR,  // (wake: kwk)
   KT_WAITING, KT_GOT, KT_RSTAT, KT_RHINT, KT_RVAL, KT_OP, KT_KEY, KT_ELEM,
   KT_KIND,  // 1 = generic_test partitioner (KT_PERM: its shuffled `all`, 4 bits per server)
   KT_PERM,
@@ -228,7 +229,7 @@ constexpr uint32_t kws(uint32_t nthr) { return (nthr + 1u) & ~1u; }
 // tester frame record (tester() in mr_kernel.hip): pc | helper << 24, result, locals l[0..7],
 // helper frame h[0..4], u64 argument hv — 17 words in five 16-B quads, loaded and stored whole
 constexpr uint32_t TF_Q = 5;
-constexpr uint32_t PROF_SLOTS = 64;
+constexpr uint32_t PROF_SLOTS = 96;  // 64..85: pool_kernel statistics (MR_PROF, tools/prof.py)
 // election-safety term bitmap (MR_F_SAFETY): terms 0..LED_TERMS-1; a leader elected in a
 // later term is a simulator limit (MR_FAIL_SIM_CAPACITY); figure_8 peaks at term 177
 constexpr uint32_t LED_W = 64, LED_TERMS = 32 * LED_W;

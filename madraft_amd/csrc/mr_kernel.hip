@@ -133,6 +133,12 @@ static_assert(STEP_BLOCK == 64, "step_kernel's lane mapping assumes one 64-lane 
 #define MR_POOL 0
 #endif
 static_assert(!MR_POOL || MR_KEY32, "the pool kernel keeps 32-bit message keys");
+#ifndef MR_POOL_AEK  // pool bins: only AppendEntries requests that carry entries in the AE bin
+#define MR_POOL_AEK 0
+#endif
+#ifndef MR_POOL_BINS  // pool bins beyond tester / AppendEntries request / other (mr_pool.inc PK_*)
+#define MR_POOL_BINS 0
+#endif
 constexpr uint32_t POOL_WAVES = 8, POOL_SLOTS = 64 * POOL_WAVES;
 using lkey_t = std::conditional_t<MR_KEY32 != 0, uint32_t, uint64_t>;
 constexpr lkey_t LKEY_FREE = ~lkey_t(0);
@@ -655,7 +661,10 @@ DI int net_send(const Dev& D, X& x, uint32_t src, uint32_t& nctr, uint32_t dst, 
   if constexpr (MR_KEY32) {
     // pool kernels (Raft-only, dst < 8): bit 3 marks an AppendEntries request, the event kind
     // the pool bins by (pool_kind); dst is key & 7 there
-    const uint32_t lo = MR_POOL && type == M_AE_REQ ? dst | 8u : dst;
+    const uint32_t lo = !MR_POOL ? dst
+                        : type == M_AE_REQ && (k || !MR_POOL_AEK) ? dst | 8u
+                        : (MR_POOL_BINS & 1) && (type == M_RV_REQ || type == M_RV_REP) ? dst | 16u
+                                                                                      : dst;
     LK(slot) = (t << 5) | lo;
     // every message in flight has a smaller seq: a new one is earliest only by time
     if (t < (uint32_t)(x.mmin >> 32)) { x.mmin = ((uint64_t)t << 32) | lo; x.mslot = slot; }
@@ -1319,8 +1328,8 @@ DI void ae_load_batch(const Dev& D, const X& x, uint32_t me, const NC& d, uint32
 // than the batches they replace). Re-measured after the argument laundering (ab20): 5-server
 // kernels −0.2 / −0.8 %, the 3-server 2D kernel +2.2 %; the 15-clerk kvraft kernels +1.5 / +0.3 %
 // (ab21): on where keys are 32-bit (the 7- / 8-server kernels).
-#ifndef MR_AE_COOP
-#define MR_AE_COOP MR_KEY32
+#ifndef MR_AE_COOP  // pool kernels: off (A/B r05ab1: figure_8_unreliable_2c +2.8 %, crash +3.3 %)
+#define MR_AE_COOP (MR_KEY32 && !MR_POOL)
 #endif
 constexpr uint32_t AE_COOP_REM = 12;  // entries after the first batch an owner may hand out (LDS rows)
 DI void wave_sync_lds() {
@@ -1346,6 +1355,7 @@ DI bool ae_recv_coop(const Dev& D, X& x, uint32_t me, NC& d, uint32_t src, bool 
   const uint32_t f0 = wrote ? jr : (jp > jr ? (jp < k ? jp : k) : jr);
   const uint32_t c1 = (cnt && !wrote) ? f0 - jr : 0u;  // entries to compare
   if (cnt) { fw[lane] = f0; bw[lane] = ~0u; }
+  wave_sync_lds();  // the owners' words are set before any helper's atomic min on them
   const uint64_t act = __ballot(1);
   const uint32_t nh = (uint32_t)__popcll(act);
   const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(act >> 32),

@@ -29,7 +29,7 @@ import csv, glob, sys, collections, json
 a = collections.defaultdict(float)
 for p in glob.glob(sys.argv[1] + "/**/run_counter_collection.csv", recursive=True):
     for r in csv.DictReader(open(p)):
-        if "step_kernel" in r["Kernel_Name"]:
+        if "step_kernel" in r["Kernel_Name"] or "pool_kernel" in r["Kernel_Name"]:
             a[r["Counter_Name"]] += float(r["Counter_Value"])
 ev = None
 for line in open(sys.argv[1] + ".log"):

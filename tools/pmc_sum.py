@@ -29,7 +29,7 @@ disp = {}
 for p in sorted(glob.glob(f"{a.dir}/p*/run_counter_collection.csv")):
     ids, names = set(), set()
     for r in csv.DictReader(open(p)):
-        if "step_kernel" not in r["Kernel_Name"]:
+        if "step_kernel" not in r["Kernel_Name"] and "pool_kernel" not in r["Kernel_Name"]:
             continue
         agg[r["Counter_Name"]] += float(r["Counter_Value"])
         ids.add(r["Dispatch_Id"])
