@@ -9,12 +9,25 @@ import time
 from . import _abi, sim, trace
 
 
+# test bodies that switch the net back to reliable part-way (tests.rs:680 unreliable_agree_2c
+# before join_all and the final one(); tests.rs:832 internal_churn before the final one()):
+# their sends have no single mode, so a log of them must carry it per line (or be a raw log)
+MIXED_MODE = {"unreliable_agree_2c", "unreliable_churn_2c"}
+
+
 def net_mode(test, unreliable_flag):
     """The network mode a replayed log's sends were drawn under when a line does not say:
-    `--unreliable` (MR_F_UNRELIABLE from the tester's start), else the test body's own mode —
-    the tests named *unreliable* switch the net to unreliable (tester.rs:127-137), the others
-    run it reliable. A line's own "unreliable" field still wins (trace.decisions_from_events)."""
-    return bool(unreliable_flag) or "unreliable" in test
+    `--unreliable` (MR_F_UNRELIABLE from the tester's start: every send unreliable), else the
+    test body's own single mode — the tests named *unreliable* that stay unreliable to the end
+    (figure_8_unreliable_2c tests.rs:692, snap_common's unreliable 2D tests :864) send every
+    message unreliably, the others reliably. For the tests that switch modes (MIXED_MODE) there
+    is no single answer: None, so trace.decisions_from_events rejects a send line without its
+    own "unreliable" field instead of decoding it under the wrong latency range and loss draw."""
+    if unreliable_flag:
+        return True
+    if test in MIXED_MODE:
+        return None
+    return "unreliable" in test
 
 
 def main():

@@ -68,17 +68,9 @@ enum : uint32_t { C64_FREE, C64_DIGEST, C64_MMIN, C64_TV, C64_FREE1 = C64_TV + T
 // consecutive words of one field), or, with MR_CS_MAJOR=1 (an A/B option, measured -5 %),
 // cluster-major records cs32[c][CS_STRIDE] / cs64[c][C64_STRIDE]. The host reads rows through
 // these index macros.
-#ifndef MR_CS_MAJOR
-#define MR_CS_MAJOR 0
-#endif
 constexpr uint32_t CS_STRIDE = (CS__N + 3u) & ~3u, C64_STRIDE = (C64__N + 1u) & ~1u;
-#if MR_CS_MAJOR
-#define CS_IDX(f, c, C) ((size_t)(c) * CS_STRIDE + (f))
-#define C64_IDX(f, c, C) ((size_t)(c) * C64_STRIDE + (f))
-#else
 #define CS_IDX(f, c, C) ((size_t)(f) * (C) + (c))
 #define C64_IDX(f, c, C) ((size_t)(f) * (C) + (c))
-#endif
 // nd32 [C][n][NREC]: one 128-B record per node. Words 0..11 are the scalars
 // an event loads / stores as a block (load_node), 12..13 the pending payload
 // range, 14..15 the snapshot value (u64), 16..23 next[p], 24..31 match[p]

@@ -66,9 +66,7 @@ struct X {
   uint32_t lmask;        // servers whose stored role is leader (kept by store_node)
   uint64_t free_mask[MW], digest, mmin;
   uint32_t timer[NB];  // node timers (election / heartbeat deadline), INF_T = none
-#if !MR_CNT_MEM
   uint32_t cnt[CNT__N];  // pool_kernel: the lane's sums over its events (per cluster: POOL_CNT)
-#endif
   uint32_t ls;  // pool_kernel: the cluster's pool slot (its LDS column)
 };
 
@@ -87,14 +85,11 @@ struct X {
 // message keys of the lane's cluster live in LDS during a launch: [slot][lane],
 // so a wave's 64 lanes read 64 consecutive u64 (conflict-free). Free slots hold
 // ~0, so the earliest-message scan is a branch-free min over all M slots.
-// lanes per block: 64 (A/B below; 256 message slots of keys need it to fit the 160 KiB of LDS)
-#ifndef MR_BLOCK
-#define MR_BLOCK 64  // A/B round 2 (with AC 4): configs 2-4 +2.4-10 %, config 5 -1 % (r02_s2r)
-#endif
-constexpr uint32_t STEP_BLOCK = MW > 2 ? 64 : MR_BLOCK;
-// the step kernel maps lane l < lpw of block b to cluster b * lpw + l (lanes_per_wave): one
-// 64-lane wave per block, which the capacity math (cap * lpw / 64) assumes too
-static_assert(STEP_BLOCK == 64, "step_kernel's lane mapping assumes one 64-lane wave per block");
+// lanes per block: 64 — one wave (A/B round 2 against 128: configs 2-4 +2.4-10 %, config 5 -1 %,
+// r02_s2r; 256 message slots of keys need it to fit the 160 KiB of LDS). The step kernel maps
+// lane l < lpw of block b to cluster b * lpw + l (lanes_per_wave), which the capacity math
+// (cap * lpw / 64) assumes too
+constexpr uint32_t STEP_BLOCK = 64;
 // MR_KEY32: a 32-bit LDS key t << 5 | dst (t < 2^27 - 1, SEMANTICS §4); the (rare) tie of
 // two messages at the same t is broken by their sequence numbers, kept in the message
 // record (word MF_PAD). Otherwise a 64-bit key (t << 32 | seq << 6 | ae << 5 | dst).
@@ -105,26 +100,11 @@ static_assert(STEP_BLOCK == 64, "step_kernel's lane mapping assumes one 64-lane 
 // (results do not depend on it) for the Raft-only kernels with 64-bit keys whose test body does
 // not restart servers (restarts_servers, mr_dev.h). A/B (profiles/r03_ab_round3.txt):
 // figure_8_unreliable_2c +6.5 %, fail_agree_2b 0; with restarts (figure_8_unreliable_crash) -9 %
-// and in the kvraft kernels (unreliable_3a) -7 %, for every per-wave threshold tried
-#ifndef MR_AE_CLASS
-#define MR_AE_CLASS 1
-#endif
-#ifndef MR_AE_NUM  // A/B: 1/2 135.4 ms, 1/3 136.1, 1/4 138.2, 2/3 139.3, off 144.7
-#define MR_AE_NUM 1
-#define MR_AE_DEN 2
-#endif
-#ifndef MR_AE_K0  // heartbeats (no entries) in the AE sub-class too
-#define MR_AE_K0 1
-#endif
-#ifndef MR_AE_KMIN  // A/B: only AppendEntries with at least this many entries in the sub-class
-#define MR_AE_KMIN 0
-#endif
-#ifndef MR_AE_OTHERS  // defer only while at least this many other node events run (A/B: 0
-#define MR_AE_OTHERS 32  // 132.4, 32 131.65, 40 134.9, 48 139.75 ms on figure_8_unreliable_2c)
-#endif
-#ifndef MR_HB_CLASS  // leaders' heartbeat timers as a sub-class of their own (same rule)
-#define MR_HB_CLASS 0
-#endif
+// and in the kvraft kernels (unreliable_3a) -7 %, for every per-wave threshold tried. The
+// deliveries wait while they are under 1/2 of the wave's node events (A/B: 1/2 135.4 ms, 1/3
+// 136.1, 1/4 138.2, 2/3 139.3, off 144.7) and at least AE_OTHERS other node events run (A/B:
+// 0 132.4, 32 131.65, 40 134.9, 48 139.75 ms on figure_8_unreliable_2c)
+constexpr uint32_t AE_OTHERS = 32;
 // MR_POOL: the cluster-pool kernel (pool_kernel below): a workgroup of
 // POOL_WAVES waves shares a pool of POOL_SLOTS clusters whose run state lives in LDS; a wave
 // takes up to 64 ready clusters whose next event is of one kind (the bins). Its translation
@@ -133,12 +113,6 @@ static_assert(STEP_BLOCK == 64, "step_kernel's lane mapping assumes one 64-lane 
 #define MR_POOL 0
 #endif
 static_assert(!MR_POOL || MR_KEY32, "the pool kernel keeps 32-bit message keys");
-#ifndef MR_POOL_AEK  // pool bins: only AppendEntries requests that carry entries in the AE bin
-#define MR_POOL_AEK 0
-#endif
-#ifndef MR_POOL_BINS  // pool bins beyond tester / AppendEntries request / other (mr_pool.inc PK_*)
-#define MR_POOL_BINS 0
-#endif
 constexpr uint32_t POOL_WAVES = 8, POOL_SLOTS = 64 * POOL_WAVES;
 using lkey_t = std::conditional_t<MR_KEY32 != 0, uint32_t, uint64_t>;
 constexpr lkey_t LKEY_FREE = ~lkey_t(0);
@@ -191,18 +165,9 @@ __shared__ unsigned long long s_prof[MR_POOL ? POOL_WAVES : 1][2 * P__N + 1];
 // ---------------------------------------------------------------- helpers
 // per-cluster statistics counters: in registers, or (MR_CNT_MEM) updated in
 // place with fire-and-forget atomics so they hold no registers
-#ifndef MR_CNT_MEM
-#define MR_CNT_MEM 0
-#endif
-#if MR_CNT_MEM
-#define CNT_GET(k) CS(CS_CNT + (k))
-#define CADD(k, v) __hip_atomic_fetch_add(&CS(CS_CNT + (k)), (uint32_t)(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-#define CMAX(k, v) __hip_atomic_fetch_max(&CS(CS_CNT + (k)), (uint32_t)(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-#else
 #define CADD(k, v) (x.cnt[k] += (v))
 #define CNT_GET(k) x.cnt[k]
 #define CMAX(k, v) do { uint32_t v_ = (v); if (v_ > x.cnt[k]) x.cnt[k] = v_; } while (0)
-#endif
 // node flag word: role[0:2) voted[4:8) (15 = none) inc[8:16) votes[16:24)
 DI uint32_t f_role(uint32_t f) { return f & 3u; }
 DI uint32_t f_voted(uint32_t f) { return (f >> 4) & 15u; }
@@ -234,23 +199,11 @@ DI void set_timer(X& x, uint32_t d, uint32_t t) {
 __device__ __forceinline__ uint2 philox2(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t k0,
                                       uint32_t k1) {
   uint32_t c3 = 0;
-#ifdef MR_DEV_CHEAP_RNG  // timing experiments only: NOT the simulator's RNG (breaks parity)
-  c0 = (c0 ^ k0) * 0x9E3779B9u ^ (c1 + k1) * 0x85EBCA6Bu ^ c2 * 0xC2B2AE35u;
-  return make_uint2(c0, c0 * 0x27D4EB2Fu + c2);
-#endif
-#ifndef MR_PHILOX_MAD64  // each round's two products as 64-bit v_mad_u64_u32 (A/B: DESIGN.md §6.6)
-#define MR_PHILOX_MAD64 1
-#endif
 #pragma unroll
   for (int r = 0; r < 10; r++) {
-#if MR_PHILOX_MAD64
     const uint64_t p0 = (uint64_t)c0 * 0xD2511F53u, p1 = (uint64_t)c2 * 0xCD9E8D57u;
     const uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
     const uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
-#else
-    uint32_t hi0 = __umulhi(0xD2511F53u, c0), lo0 = 0xD2511F53u * c0;
-    uint32_t hi1 = __umulhi(0xCD9E8D57u, c2), lo1 = 0xCD9E8D57u * c2;
-#endif
     uint32_t n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
     c0 = n0; c1 = lo1; c2 = n2; c3 = lo0;
     k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
@@ -297,14 +250,6 @@ DI void philox(const Dev& D, X& x, uint32_t c0, uint32_t c1, uint32_t c2, uint32
   const uint2 w = philox2(c0, c1, c2, (uint32_t)seed, (uint32_t)(seed >> 32));
   w0 = w.x;
   w1 = w.y;
-#ifdef MR_DEV_DUP_PHILOX  // timing only: every draw computed twice (the copy's result is discarded)
-  {
-    uint32_t z = 0, k1 = (uint32_t)(seed >> 32) ^ 0x5bd1e995u;
-    asm volatile("" : "+v"(z), "+v"(k1));
-    const uint2 w2 = philox2(c0, c1, c2, (uint32_t)seed, k1);
-    w0 ^= (w2.x ^ w2.y) & z;
-  }
-#endif
 }
 DI size_t logi(const Dev& D, const X& x, uint32_t d, uint32_t i) {
   return ((size_t)x.c * D.n + d) * D.log_cap + (i & (D.log_cap - 1u));
@@ -412,16 +357,6 @@ __device__ __forceinline__ uint64_t fnv8(uint64_t h, uint32_t w0, uint32_t w1, u
 DI void rec8(const Dev& D, X& x, uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3, uint32_t w4,
              uint32_t w5, uint32_t w6, uint32_t w7) {
   x.digest = fnv8(x.digest, w0, w1, w2, w3, w4, w5, w6, w7);
-#ifdef MR_DEV_DUP_DIGEST  // timing only: the digest computed twice
-  {
-    uint64_t h2 = x.digest;
-    asm volatile("" : "+v"(h2));
-    h2 = fnv8(h2, w0, w1, w2, w3, w4, w5, w6, w7);
-    uint64_t z = 0;
-    asm volatile("" : "+v"(z));
-    x.digest ^= h2 & z;
-  }
-#endif
   if (x.c < D.trace_clusters && x.trace_n < D.trace_cap) {
     uint32_t* p = reinterpret_cast<uint32_t*>(D.trace + (size_t)x.c * D.trace_cap + x.trace_n);
     p[0] = w0; p[1] = w1; p[2] = w2; p[3] = w3; p[4] = w4; p[5] = w5; p[6] = w6; p[7] = w7;
@@ -436,47 +371,16 @@ DI void rec_node(const Dev& D, X& x, uint32_t cls, uint32_t kind, uint32_t d, ui
        n.applied, n.last, n.snap);
 }
 
-// a node event's trace record, taken as the event ends and appended by the step loop: one
-// copy of the record path (FNV digest, trace store) serves deliveries, drops and timer events,
-// so a wave whose lanes took different exits runs it once (MR_REC_ONCE)
-#ifndef MR_REC_ONCE
-#define MR_REC_ONCE 0
-#endif
-struct NR {
-  uint32_t w1, aux, term, commit, applied, last, snap;
-  bool on;
-};
-DI void nr_set(const Dev& D, X& x, NR& r, uint32_t cls, uint32_t kind, uint32_t d, uint32_t aux,
-               const NC& n) {
-#if MR_REC_ONCE
-  const uint32_t role = bit(x.alive, d) ? f_role(n.f) : R_DOWN;
-  r = NR{cls | (kind << 8) | (d << 16) | (role << 24), aux, n.term, n.commit, n.applied, n.last,
-         n.snap, true};
-#else
-  rec_node(D, x, cls, kind, d, aux, n);
-#endif
-}
-
 DI void rec_simple(const Dev& D, X& x, uint32_t cls, uint32_t kind) {
   rec8(D, x, x.now, cls | (kind << 8) | (0xFFu << 16), x.msgs_sent, 0, 0, 0, 0, 0);
 }
 
 // A verdict stops the cluster (a Rust panic): its trace record (class 3) is the event's last.
-// Handlers return as soon as x.code leaves MR_RUNNING, before any further observable effect,
-// and nothing they do after it changes x.now or x.msgs_sent, so the record is appended once,
-// where the step loop ends the event (fail_flush) — one copy of the record path instead of one
-// inlined at each of the ~100 panic sites (MR_FAIL_DEFER; A/B in DESIGN.md §6.8)
-#ifndef MR_FAIL_DEFER
-#define MR_FAIL_DEFER 0
-#endif
+// Handlers return as soon as x.code leaves MR_RUNNING, before any further observable effect.
 DI void fail(const Dev& D, X& x, uint32_t code) {
   if (x.code != RUN) return;
   x.code = code;
-  if (!MR_FAIL_DEFER) rec_simple(D, x, 3, code);
-}
-// the deferred verdict record of an event that ended the cluster (t_end records MR_PASS itself)
-DI void fail_flush(const Dev& D, X& x) {
-  if (MR_FAIL_DEFER && x.code != RUN && x.code != MR_PASS) rec_simple(D, x, 3, x.code);
+  rec_simple(D, x, 3, code);
 }
 
 // ---------------------------------------------------------------- timers / net
@@ -486,15 +390,10 @@ DI void reset_timer(const Dev& D, X& x, uint32_t d, NC& n) {  // raft.rs:260-263
   set_timer(x, d, x.now + u_range(w0, D.elo, D.ehi));
 }
 
-#ifndef MR_RESCAN_OCC  // scan only the occupied slots (A/B: DESIGN.md §6)
-#define MR_RESCAN_OCC 1
-#endif
 // the earliest-message rescan four occupied slots per trip, their LDS reads issued together:
 // after the argument laundering (ab20) figure_8_unreliable_2c +1.2 %, crash +0.6 %, C5 +1 %
 // (ab11), the 3-server 2D kernel −1.3 % (ab20): on for 64-bit keys (the 3- / 5-server kernels)
-#ifndef MR_RESCAN_X4
-#define MR_RESCAN_X4 (!MR_KEY32)
-#endif
+constexpr bool RESCAN_X4 = !MR_KEY32;
 DI void rescan_min(const Dev& D, X& x) {
   if constexpr (MR_KEY32) {
     uint32_t bt = ~0u, bk = ~0u, bs = 0;
@@ -503,7 +402,7 @@ DI void rescan_min(const Dev& D, X& x) {
     for (uint32_t w = 0; w < MW; w++) {
       const uint32_t mw = D.M > 64u * w ? D.M - 64u * w : 0u;
       uint64_t occ = ~x.free_mask[w] & (mw >= 64 ? ~0ull : ((1ull << mw) - 1ull));
-      if constexpr (MR_RESCAN_X4) {  // four occupied slots per trip, their LDS reads issued together
+      if constexpr (RESCAN_X4) {  // four occupied slots per trip, their LDS reads issued together
         while (occ) {
           uint32_t s4[4];
           bool v4[4];
@@ -554,7 +453,7 @@ DI void rescan_min(const Dev& D, X& x) {
   }
   uint64_t best = ~0ull;
   uint32_t bs = 0;
-  if constexpr (MR_RESCAN_X4 && MW == 1) {
+  if constexpr (RESCAN_X4 && MW == 1) {
     uint64_t occ = ~x.free_mask[0] & (D.M >= 64 ? ~0ull : ((1ull << D.M) - 1ull));
     while (occ) {
       uint32_t s4[4];
@@ -570,7 +469,7 @@ DI void rescan_min(const Dev& D, X& x) {
       for (uint32_t q = 0; q < 4; q++)
         if (k4[q] < best) { best = k4[q]; bs = s4[q]; }
     }
-  } else if constexpr (MR_RESCAN_OCC && MW == 1) {
+  } else if constexpr (MW == 1) {
     uint64_t occ = ~x.free_mask[0] & (D.M >= 64 ? ~0ull : ((1ull << D.M) - 1ull));
     while (occ) {
       const uint32_t s = (uint32_t)__builtin_ctzll(occ);
@@ -605,9 +504,6 @@ DI bool link_cut(const Dev& D, X& x, uint32_t a, uint32_t b) {
 // that clog (its `reach` mask folds in the connect state and the cut links), and records a
 // capacity verdict itself where the loop exits, so the loop body carries no clog test and no
 // inlined copy of the verdict record
-#ifndef MR_SEND_LEAN
-#define MR_SEND_LEAN 1
-#endif
 DI int net_send(const Dev& D, X& x, uint32_t src, uint32_t& nctr, uint32_t dst, uint32_t type,
                 uint32_t inc, uint32_t term, uint32_t a, uint32_t b, uint32_t c, uint64_t v,
                 uint32_t k, uint32_t ent = NONE, bool lean = false) {
@@ -662,9 +558,9 @@ DI int net_send(const Dev& D, X& x, uint32_t src, uint32_t& nctr, uint32_t dst, 
     // pool kernels (Raft-only, dst < 8): bit 3 marks an AppendEntries request, the event kind
     // the pool bins by (pool_kind); dst is key & 7 there
     const uint32_t lo = !MR_POOL ? dst
-                        : type == M_AE_REQ && (k || !MR_POOL_AEK) ? dst | 8u
-                        : (MR_POOL_BINS & 1) && (type == M_RV_REQ || type == M_RV_REP) ? dst | 16u
-                                                                                      : dst;
+                        : type == M_AE_REQ ? dst | 8u
+                        : type == M_RV_REQ || type == M_RV_REP ? dst | 16u
+                                                               : dst;
     LK(slot) = (t << 5) | lo;
     // every message in flight has a smaller seq: a new one is earliest only by time
     if (t < (uint32_t)(x.mmin >> 32)) { x.mmin = ((uint64_t)t << 32) | lo; x.mslot = slot; }
@@ -672,7 +568,7 @@ DI int net_send(const Dev& D, X& x, uint32_t src, uint32_t& nctr, uint32_t dst, 
     // bit 5: AppendEntries request (the step loop's AE sub-class, MR_AE_CLASS); below the
     // unique seq, so it never decides the order
     const uint64_t key = ((uint64_t)t << 32) | (seq << 6) |
-                         (type == M_AE_REQ && (MR_AE_K0 || k) && k >= MR_AE_KMIN ? 32u : 0u) | dst;
+                         (type == M_AE_REQ ? 32u : 0u) | dst;
     LK(slot) = key;
     if (key < x.mmin) { x.mmin = key; x.mslot = slot; }
   }
@@ -695,18 +591,11 @@ constexpr uint32_t LAT_BOUND_US = 27000u;
 // a node event's pending payload range (NF_PLO, NF_PHI) loaded with its record (before round 3's
 // second half this switch was tested before its definition and so was always off: pend_note and
 // the AppendEntries write guard reloaded the range after the sends, waiting on their stores)
-#ifndef MR_PLO_EARLY
-#define MR_PLO_EARLY 1
-#endif
 DI void pend_note(const Dev& D, X& x, uint32_t me, NC& d, uint32_t lo, uint32_t hi,
                   uint32_t olo_early = 0, uint32_t ohi_early = 0) {
   uint32_t plo = lo, phi = hi;
   if (x.now <= d.pexp) {
-#if MR_PLO_EARLY  // loaded with the node record (unchanged in the event while x.now <= pexp)
     uint32_t olo = olo_early, ohi = ohi_early;
-#else
-    uint32_t olo = ND(NF_PLO, me), ohi = ND(NF_PHI, me);
-#endif
     if (olo <= ohi) { plo = olo < lo ? olo : lo; phi = ohi > hi ? ohi : hi; }
   }
   ND(NF_PLO, me) = plo;
@@ -755,23 +644,11 @@ DI void guard_log_write(const Dev& D, X& x, uint32_t L, uint32_t& pexp, uint32_t
 }
 
 // ---------------------------------------------------------------- tester storage
-#ifndef MR_AC
-#define MR_AC 4  // A/B round 2: 4 vs 8 +1.7 % figure_8 with 64-lane blocks (profiles/r02_ab_configs.txt r02_s2r)
-#endif
-constexpr uint32_t AC = MR_AC;  // entries per batch of independent loads in log walks
-#ifndef MR_SEND_EARLY  // a leader's append-term loads issued before the applier (A/B in DESIGN.md §6)
-#define MR_SEND_EARLY 1
-#endif
-#ifndef MR_AP_PIPE  // software-pipelined applier batches (node_apply); A/B in DESIGN.md §6
-#define MR_AP_PIPE 1
-#endif
-#ifndef MR_KV_PRE  // KV applier: a batch's key records loaded with the batch (node_apply)
-#define MR_KV_PRE 0
-#endif
-#ifndef MR_AC_APPLY  // pipelined: two batches of 5 in flight fit the registers (8: spills)
-#define MR_AC_APPLY (MR_AP_PIPE ? 5 : 8)
-#endif
-constexpr uint32_t AC_APPLY = MR_AC_APPLY;  // entries per batch in the applier
+// entries per batch of independent loads in log walks (A/B round 2: 4 vs 8 +1.7 % figure_8 with
+// 64-lane blocks, profiles/r02_ab_configs.txt r02_s2r; round 3: 2 / 3 / 5 / 6 / 8 -7.0 / -1.7 /
+// -3.3 / -3.3 / -20 %)
+constexpr uint32_t AC = 4;
+constexpr uint32_t AC_APPLY = 5;  // entries per batch in the applier
 DI void storage_snapshot(const Dev& D, X& x, uint32_t i, uint32_t& slen, uint32_t idx) {  // tester.rs:399-402
   if (idx >= D.apply_cap) { fail(D, x, MR_FAIL_SIM_CAPACITY); return; }
   uint32_t nl = idx + 1;
@@ -813,9 +690,6 @@ enum : uint32_t { SEND_NONE = 0, SEND_REPLY, SEND_APPEND, SEND_VOTE };
 // VGPR lanes, are reloaded whole (16 v_readlane) wherever one of their fields is used. On it:
 // the node event (MR_NE_LAUNDER, headline kernel 1 662 -> 988 v_readlane, VALU -9 %) or, as an
 // A/B, only the applier (MR_AP_LAUNDER). Fields the scenario fixes at compile time are left alone.
-#ifndef MR_AP_LAUNDER
-#define MR_AP_LAUNDER 0
-#endif
 template <class T>
 DI T* glp(T* p) {
   uint64_t v = (uint64_t)(uintptr_t)p;
@@ -826,61 +700,33 @@ DI uint32_t glu(uint32_t v) {
   asm volatile("" : "+s"(v));
   return v;
 }
-#ifndef MR_LAUNDER_S  // only the fields scenario S has (its arrays and services), not a runtime test
-#define MR_LAUNDER_S 1
-#endif
 template <uint32_t S>
 DI Dev dev_launder(const Dev& D0) {
   Dev D = D0;
   D.log = glp(D0.log); D.stor = glp(D0.stor); D.cs32 = glp(D0.cs32); D.nd32 = glp(D0.nd32);
-  if (MR_LAUNDER_S ? is_svc(S) : D0.kv32 != nullptr) D.kv32 = glp(D0.kv32);
-  if (MR_LAUNDER_S ? kv_gen(S).maxraft > 0 : D0.kvs32 != nullptr) D.kvs32 = glp(D0.kvs32);
-  if (MR_LAUNDER_S ? kv_gen(S).maxraft > 0 : D0.kring != nullptr) D.kring = glp(D0.kring);
+  if (is_svc(S)) D.kv32 = glp(D0.kv32);
+  if (kv_gen(S).maxraft > 0) { D.kvs32 = glp(D0.kvs32); D.kring = glp(D0.kring); }
   D.trace = glp(D0.trace);
   D.apply_cap = glu(D0.apply_cap); D.log_cap = glu(D0.log_cap); D.bugs = glu(D0.bugs);
   D.trace_clusters = glu(D0.trace_clusters); D.trace_cap = glu(D0.trace_cap);
-#ifndef MR_LAUNDER_ALL  // every field the node event reads, not only the applier's
-#define MR_LAUNDER_ALL 1
-#endif
-  if (MR_LAUNDER_ALL) {
-    D.ms32 = glp(D0.ms32); D.pay = glp(D0.pay); D.tmr = glp(D0.tmr);
-    if (D0.led) D.led = glp(D0.led);
-    if (MR_LAUNDER_S ? is_kv(S) : D0.lin32 != nullptr) D.lin32 = glp(D0.lin32);
-    if (MR_LAUNDER_S ? nthr(S) > 0 : D0.kt32 != nullptr) D.kt32 = glp(D0.kt32);
-    if (MR_LAUNDER_S ? nthr(S) > 0 : D0.kwk != nullptr) D.kwk = glp(D0.kwk);
-    D.seed0 = ((uint64_t)glu((uint32_t)(D0.seed0 >> 32)) << 32) | glu((uint32_t)D0.seed0);
-    D.M = glu(D0.M); D.K = glu(D0.K); D.hb = glu(D0.hb); D.elo = glu(D0.elo); D.ehi = glu(D0.ehi);
-    D.safety = glu(D0.safety); D.max_events = glu(D0.max_events);
-  }
+  D.ms32 = glp(D0.ms32); D.pay = glp(D0.pay); D.tmr = glp(D0.tmr);
+  if (D0.led) D.led = glp(D0.led);
+  if (is_kv(S)) D.lin32 = glp(D0.lin32);
+  if (nthr(S) > 0) { D.kt32 = glp(D0.kt32); D.kwk = glp(D0.kwk); }
+  D.seed0 = ((uint64_t)glu((uint32_t)(D0.seed0 >> 32)) << 32) | glu((uint32_t)D0.seed0);
+  D.M = glu(D0.M); D.K = glu(D0.K); D.hb = glu(D0.hb); D.elo = glu(D0.elo); D.ehi = glu(D0.ehi);
+  D.safety = glu(D0.safety); D.max_events = glu(D0.max_events);
   return D;
 }
 
 template <uint32_t S>
-DI void node_apply(const Dev& Darg, X& x, uint32_t me, NC& d, uint32_t& kvready) {
-  const Dev D = MR_AP_LAUNDER ? dev_launder<S>(Darg) : Darg;
+DI void node_apply(const Dev& D, X& x, uint32_t me, NC& d, uint32_t& kvready) {
   constexpr bool KV = is_svc(S);
   const bool snapmode = (x.netmode >> 1) & 1u;
   SE* const sb = D.stor + (size_t)x.c * D.apply_cap;
   uint32_t len = d.slen;
   uint32_t pm = 0;  // KV: the server's occupied pending-request slots (kv_apply)
   if constexpr (KV) pm = KVP(me)[KVR_PMASK];
-#ifndef MR_KV_PIDX  // KV: the pending slots' log indices read once per applier visit (A/B round 4)
-#define MR_KV_PIDX 0
-#endif
-  // each pending slot's log index, loaded with the mask (a freed slot's is 0, never an applied
-  // index; the indices do not change while the applier runs): an entry's answers then load only
-  // the slots waiting for its index, not a round trip per occupied slot
-  uint32_t pidx[KV_PEND];
-#pragma unroll
-  for (uint32_t q = 0; q < KV_PEND; q++) pidx[q] = (KV && MR_KV_PIDX) ? KVP(me)[KVR_PEND + 8u * q] : 0u;
-  auto pwait = [&](uint32_t i) -> uint32_t {  // the occupied slots waiting for index i
-    if (!(KV && MR_KV_PIDX)) return pm;
-    uint32_t mm = 0;
-#pragma unroll
-    for (uint32_t q = 0; q < KV_PEND; q++) mm |= (pidx[q] == i ? 1u : 0u) << q;
-    return pm & mm;
-  };
-#if MR_AP_PIPE
   // software-pipelined: batch b + 1's loads are issued before batch b's checker stores, so
   // they do not wait behind them on vmcnt (disjoint indices: a batch never reads what an
   // earlier one wrote; the log is not written here)
@@ -907,56 +753,6 @@ DI void node_apply(const Dev& Darg, X& x, uint32_t me, NC& d, uint32_t& kvready)
 #pragma unroll
     for (uint32_t j = 0; j < AC_APPLY; j++) { ce[j] = e[j]; cm[j] = m[j]; csv[j] = sv[j]; }
     if (i0 + AC_APPLY <= d.commit) load_batch(i0 + AC_APPLY);
-    // KV (not the controller): the batch's key records and dedup words as one batch of loads
-    // (the batch's commands are known here); an entry whose key or clerk an earlier entry of
-    // the batch shares reads them after that entry's stores instead (kv_apply loads)
-    constexpr bool PRE = KV && !is_ctrl(S) && !kv_gen(S).lin && MR_KV_PRE;
-    // generic_test_linearizability's servers (SEMANTICS §9b): each entry's key-record quad, the
-    // clerk's dedup word and the state word of the client it names, for the whole batch at once
-    // (an entry sharing a key or a clerk with an earlier one of the batch reads them after that
-    // entry's stores instead) — one round trip per batch instead of one per entry. Measured
-    // round 4 (profiles/r04_ab_round4.txt, 65536 clusters): parity-green but 3a 656 -> 712 ms,
-    // 3b 804 -> 807 ms (the batch's 5x6 live words cost more than the round trips they save) — off
-#ifndef MR_LIN15_PRE
-#define MR_LIN15_PRE 0
-#endif
-    constexpr bool PRE15 = KV && !is_ctrl(S) && kv_gen(S).lin && MR_LIN15_PRE;
-    uint4 pka[AC_APPLY], pkb[AC_APPLY];
-    uint32_t pdd[AC_APPLY], pkey[AC_APPLY], pcl[AC_APPLY];
-    if constexpr (PRE) {
-      const uint32_t* kp = KVP(me);
-#pragma unroll
-      for (uint32_t j = 0; j < AC_APPLY; j++) {
-        const uint32_t i = i0 + j;
-        const bool ok = i <= d.commit && i < D.apply_cap;
-        const uint64_t v = ce[j].val;
-        const uint32_t key = (uint32_t)(v >> 55) & 63u, cl = (uint32_t)(v >> 48) & 127u;
-        pkey[j] = ok ? key : 64u + j;  // no match for entries past the batch
-        pcl[j] = ok ? cl : 128u + j;
-        const uint4* kq = reinterpret_cast<const uint4*>(kp + KVR_KEYS + KV_KW * key);
-        pka[j] = ok ? kq[0] : uint4{};
-        pkb[j] = ok ? kq[1] : uint4{};
-        pdd[j] = ok ? kp[KVR_DEDUP + cl] : 0u;
-      }
-    }
-    if constexpr (PRE15) {
-      const uint32_t* kp = KVP(me);
-#pragma unroll
-      for (uint32_t j = 0; j < AC_APPLY; j++) {
-        const uint32_t i = i0 + j;
-        const bool ok = i <= d.commit && i < D.apply_cap;
-        const uint64_t v = ce[j].val;
-        const uint32_t op = (uint32_t)(v >> 61) & 3u, key = (uint32_t)(v >> 55) & 15u;
-        const uint32_t cl = (uint32_t)(v >> 48) & 127u, elem = (uint32_t)v & 0xFFFFFFu;
-        const uint32_t cs = op == KV_GET ? elem : elem >> 19;
-        pkey[j] = ok ? key : 64u + j;  // no match for entries past the batch
-        pcl[j] = ok ? cl : 128u + j;
-        const uint32_t* kr = kp + KVR_KEYS + KV_KW15 * key;
-        pka[j] = ok ? reinterpret_cast<const uint4*>(kr)[0] : uint4{};
-        pkb[j].x = ok && cs < LIN_CLI ? kr[3 + cs] : 0u;
-        pdd[j] = ok ? kp[KVR_DEDUP + cl] : 0u;
-      }
-    }
     PROF(P_AP_LOAD);
 #pragma unroll
     for (uint32_t j = 0; j < AC_APPLY; j++) {
@@ -979,14 +775,7 @@ DI void node_apply(const Dev& Darg, X& x, uint32_t me, NC& d, uint32_t& kvready)
         CADD(CNT_SNAPSHOTS, 1u);
       }
       if constexpr (KV) {
-        bool pre = false;
-        if constexpr (PRE || PRE15) {
-          bool conf = false;
-#pragma unroll
-          for (uint32_t q = 0; q < j; q++) conf |= pkey[q] == pkey[j] || pcl[q] == pcl[j];
-          pre = !conf;
-        }
-        kv_apply<is_ctrl(S)>(D, x, me, i, ce[j].val, kvready, pwait(i), pre, pka[j], pkb[j], pdd[j]);
+        kv_apply<is_ctrl(S)>(D, x, me, i, ce[j].val, kvready, pm);
         if (x.code != RUN) return;
       }
       if constexpr (kv_gen(S).maxraft > 0) {  // the KV service snapshots (SEMANTICS §9)
@@ -1003,61 +792,6 @@ DI void node_apply(const Dev& Darg, X& x, uint32_t me, NC& d, uint32_t& kvready)
     }
     PROF(P_AP_CHECK);
   }
-#else
-  while (d.applied < d.commit) {
-    const uint32_t i0 = d.applied + 1;
-    LE e[AC_APPLY];
-    uint32_t m[AC_APPLY];
-    uint64_t sv[AC_APPLY];
-#pragma unroll
-    for (uint32_t j = 0; j < AC_APPLY; j++) {
-      const uint32_t i = i0 + j;
-      const bool ok = i <= d.commit && i < D.apply_cap;
-      e[j] = ok ? D.log[logi(D, x, me, i)] : LE{};
-      const SE s = ok ? sb[i] : SE{};
-      m[j] = s.mask;
-      sv[j] = s.val;
-    }
-    PROF(P_AP_LOAD);
-#pragma unroll
-    for (uint32_t j = 0; j < AC_APPLY; j++) {
-      const uint32_t i = i0 + j;
-      if (i > d.commit) break;
-      d.applied = i;
-      if (i >= D.apply_cap) { fail(D, x, MR_FAIL_SIM_CAPACITY); return; }
-      CADD(CNT_APPLIES, 1u);
-      if (m[j] && sv[j] != e[j].val) { fail(D, x, MR_FAIL_APPLY_MISMATCH); return; }  // tester.rs:384
-      if (i > len) { fail(D, x, MR_FAIL_APPLY_OUT_OF_ORDER); return; }  // tester.rs:393
-      if (i == len) {
-        sb[i] = SE{e[j].val, m[j] | (1u << me), e[j].term};
-        len++;
-        CMAX(CNT_MAX_INDEX, i);
-      }
-      if (snapmode && (i + 1) % 10u == 0 && i > d.snap) {  // 2D: service snapshots every 10
-        d.snapt = e[j].term;
-        d.snap = i;
-        NSV(me) = e[j].val;
-        CADD(CNT_SNAPSHOTS, 1u);
-      }
-      if constexpr (KV) {
-        kv_apply<is_ctrl(S)>(D, x, me, i, e[j].val, kvready, pwait(i));
-        if (x.code != RUN) return;
-      }
-      if constexpr (kv_gen(S).maxraft > 0) {  // the KV service snapshots (SEMANTICS §9)
-        const uint32_t sz = 32u + (f_voted(d.f) != 15u ? 9u : 1u) + 24u * (d.last - d.snap);
-        if (i % KV_SNAP_EVERY == 0 && i > d.snap && sz >= kv_gen(S).maxraft / 2) {
-          d.snapt = e[j].term;
-          d.snap = i;
-          NSV(me) = e[j].val;
-          CADD(CNT_SNAPSHOTS, 1u);
-          kv_snapshot(D, x, me, i);
-          if (x.code != RUN) return;
-        }
-      }
-    }
-    PROF(P_AP_CHECK);
-  }
-#endif
   d.slen = len;
 }
 
@@ -1080,12 +814,8 @@ DI void node_apply(const Dev& Darg, X& x, uint32_t me, NC& d, uint32_t& kvready)
 //     last: its term reaches the owner through LDS, its value goes straight to the record.
 // Helper work is found by a wave-uniform loop over the owning lanes (readlane), so lanes
 // that are not in this call never contribute a value.
-#ifndef MR_AP_COOP
-#define MR_AP_COOP 1
-#endif
 template <uint32_t S>
-DI void node_apply_coop(const Dev& Darg, X& x, uint32_t me, NC& d) {
-  const Dev D = MR_AP_LAUNDER ? dev_launder<S>(Darg) : Darg;
+DI void node_apply_coop(const Dev& D, X& x, uint32_t me, NC& d) {
   // snap_common (the 2D tests, uses_service_snapshots) runs with service snapshots:
   // t_new(snapshot = true) precedes every node event of such a batch, so the mode is the same
   // for every lane here. A scenario whose runtime mode (x.netmode bit 1, what node_apply
@@ -1267,12 +997,8 @@ DI uint32_t on_ack(const Dev& D, X& x, uint32_t me, NC& d, uint32_t p, uint32_t 
 // AC entries j.. of an AppendEntries payload (the sender's ring, or the
 // materialized copy) and the receiver's entries at their indices: their terms, and (MR_F_SAFETY
 // log matching) their commands, from one 16-B load per entry
-#ifndef MR_AE_PIPE  // A/B: AppendEntries receive batches software-pipelined (node_event)
-#define MR_AE_PIPE 0
-#endif
-#ifndef MR_AE_OWN  // 5-server kernels: yes (+0.7 %); 7 / 8: no (118 -> 4 spilled VGPRs at NB = 7)
+// MR_AE_OWN: 5-server kernels: yes (+0.7 %); 7 / 8: no (118 -> 4 spilled VGPRs at NB = 7)
 #define MR_AE_OWN (MR_NB <= 5)
-#endif
 DI void ae_load_batch(const Dev& D, const X& x, uint32_t me, const NC& d, uint32_t src, bool mat,
                       const LE* pp, uint32_t ma, uint32_t k, uint32_t j, LE (&pe)[AC],
                       uint32_t (&lt)[AC], uint64_t (&ov)[AC], uint32_t (&ors)[AC]) {
@@ -1302,7 +1028,7 @@ DI void ae_load_batch(const Dev& D, const X& x, uint32_t me, const NC& d, uint32
   }
 }
 
-// Cooperative AppendEntries receive (MR_AE_COOP). A catch-up payload carries up to K entries;
+// Cooperative AppendEntries receive (AE_COOP). A catch-up payload carries up to K entries;
 // its receiver used to walk them in batches of AC, one dependent round trip per batch, while the
 // wave's other lanes waited. The first batch is still walked by its receiver (the common
 // heartbeat or short append ends there); the entries after it, of every lane of the wave that
@@ -1328,9 +1054,9 @@ DI void ae_load_batch(const Dev& D, const X& x, uint32_t me, const NC& d, uint32
 // than the batches they replace). Re-measured after the argument laundering (ab20): 5-server
 // kernels −0.2 / −0.8 %, the 3-server 2D kernel +2.2 %; the 15-clerk kvraft kernels +1.5 / +0.3 %
 // (ab21): on where keys are 32-bit (the 7- / 8-server kernels).
-#ifndef MR_AE_COOP  // pool kernels: off (A/B r05ab1: figure_8_unreliable_2c +2.8 %, crash +3.3 %)
-#define MR_AE_COOP (MR_KEY32 && !MR_POOL)
-#endif
+// the 7- / 8-server kernels; not the pool kernels (A/B r05ab1: figure_8_unreliable_2c +2.8 %,
+// its crash variant +3.3 % without it)
+constexpr bool AE_COOP = MR_KEY32 && !MR_POOL;
 constexpr uint32_t AE_COOP_REM = 12;  // entries after the first batch an owner may hand out (LDS rows)
 DI void wave_sync_lds() {
   __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
@@ -1472,46 +1198,28 @@ DI bool ae_recv_coop(const Dev& D, X& x, uint32_t me, NC& d, uint32_t src, bool 
 // the whole node event on the laundered argument copy (dev_launder). Same-box A/B, round 4
 // (profiles/r04_ab_round4.txt ab15): figure_8_unreliable_2c 125.6 -> 121.8 ms, its crash variant
 // 67.2 -> 63.6, C5 183 -> 176, C5-lin 561 -> 528 / 690 -> 675; the tester on it too: worse
-#ifndef MR_NE_LAUNDER
-#define MR_NE_LAUNDER 1
-#endif
 template <uint32_t S>
 DI void node_event(const Dev& Darg, X& x, bool is_msg, uint32_t tnode, uint32_t slot,
-                   uint32_t seq, NR& nr) {
-  const Dev D = MR_NE_LAUNDER ? dev_launder<S>(Darg) : Darg;
+                   uint32_t seq) {
+  const Dev D = dev_launder<S>(Darg);
   constexpr bool KV = is_svc(S);  // kvraft / shard_ctrler request path
   uint32_t me = tnode, src = 0, type = 0, inc = 0, k = 0, mterm = 0, ma = 0, mb = 0, mc = 0;
   uint32_t kvready = 0;  // KV: the pending-request slots answered in this event (kv_flush)
   uint32_t hdr_bits = 0;
-#ifdef MR_DEV_PRIO  // A/B: the wave issuing an event's first loads ahead of the SIMD's other wave
-  __builtin_amdgcn_s_setprio(MR_DEV_PRIO);
-#endif
-#ifndef MR_NODE_FIRST  // the node record's loads issued before the message is decoded
-#define MR_NODE_FIRST 1
-#endif
-#if MR_NODE_FIRST
   // the server is known from the event key, so its record, next[] / match[] and pending
   // payload range are loaded together with the message (a clerk host has no record)
   const bool has_rec = !KV || me < CLERK_HOST;
   NC d = has_rec ? load_node(D, x, me) : NC{};
   PV pv;
-#ifndef MR_PEERS_LEADER  // next[] / match[] loaded only for a leader's event (A/B round 4)
-#define MR_PEERS_LEADER 1
-#endif
   // only a leader reads them (appends, acknowledgements); x.lmask mirrors the stored roles
   // (store_node), so the record's role is known without waiting for it
-  if (has_rec && (!MR_PEERS_LEADER || bit(x.lmask, me))) {
+  if (has_rec && bit(x.lmask, me)) {
     load_peers(D, x, me, pv);
   } else {
 #pragma unroll
     for (uint32_t q = 0; q < NB; q++) { pv.nx[q] = 0u; pv.mt[q] = 0u; }
   }
-#if MR_PLO_EARLY
   const uint2 prange = has_rec ? reinterpret_cast<const uint2*>(NDP(me))[NF_PLO / 2] : make_uint2(0u, 0u);
-#else
-  const uint2 prange = make_uint2(0u, 0u);
-#endif
-#endif
   if (is_msg) {
     const uint4 m0 = reinterpret_cast<const uint4*>(MSP(slot))[0];
     const uint32_t hdr = m0.x;
@@ -1529,17 +1237,6 @@ DI void node_event(const Dev& Darg, X& x, bool is_msg, uint32_t tnode, uint32_t 
       for (uint32_t w = 0; w < MW; w++) x.free_mask[w] |= (slot >> 6) == w ? 1ull << (slot & 63u) : 0ull;
     }
     x.inflight--;
-#ifdef MR_DEV_DUP_RESCAN  // timing only: the rescan done twice
-    {
-      uint64_t fm = x.free_mask[0];
-      asm volatile("" : "+v"(fm));
-      x.free_mask[0] = fm;
-      rescan_min(D, x);
-      uint64_t mm = x.mmin;
-      asm volatile("" : "+v"(mm));
-      x.mmin = mm;
-    }
-#endif
     rescan_min(D, x);
     PROF(P_DECODE);
     if constexpr (KV) {
@@ -1550,59 +1247,15 @@ DI void node_event(const Dev& Darg, X& x, bool is_msg, uint32_t tnode, uint32_t 
       }
     }
   }
-#if !MR_NODE_FIRST
-  NC d = load_node(D, x, me);
-  PV pv;
-  load_peers(D, x, me, pv);
-#if MR_PLO_EARLY
-  const uint2 prange = reinterpret_cast<const uint2*>(NDP(me))[NF_PLO / 2];
-#else
-  const uint2 prange = make_uint2(0u, 0u);
-#endif
-#endif
   PROF(P_LOAD);
-#ifndef MR_WAIT_HYGIENE
-// Loads whose first use the compiler would otherwise place after stores (the pending payload
-// range, read after the send loop; a snapshot value read inside it) make that use wait on
-// vmcnt(0), i.e. on every store issued since (vmcnt counts loads and stores in issue order):
-// the range is consumed here, with the node record, and the snapshot value is loaded where an
-// InstallSnapshot is sent (A/B in DESIGN.md §6.8)
-#define MR_WAIT_HYGIENE 1
-#endif
   uint2 prange_r = prange;
-#if MR_WAIT_HYGIENE  // opaque from here on: kept in registers, never reloaded after the sends
   asm volatile("" : "+v"(prange_r.x), "+v"(prange_r.y));
-#endif
-#ifdef MR_DEV_PRIO
-  __builtin_amdgcn_s_setprio(0);
-#endif
-#ifdef MR_DEV_EXTRA_RT  // timing only: one more dependent round trip per node event
-  {
-    uint32_t z = d.f;
-    asm volatile("" : "+v"(z));
-    z &= 0u;
-    asm volatile("" : "+v"(z));
-    const uint32_t v = NDP(me)[NF_PEXP + z];
-    asm volatile("" ::"v"(v));
-  }
-#endif
-#ifdef MR_DEV_EXTRA_VALU  // timing only: MR_DEV_EXTRA_VALU more VALU instructions per node event
-  {
-    uint32_t z = x.now;
-#pragma unroll
-    for (int i = 0; i < MR_DEV_EXTRA_VALU; i++) asm volatile("v_add_u32 %0, %0, 1" : "+v"(z));
-    asm volatile("" ::"v"(z));
-  }
-#endif
   // election-timer resets (raft.rs:260-263) are counted where the handlers call them and
   // drawn once, after the handler: the timer keeps only the last draw, each draw is keyed by
   // its own ectr (SEMANTICS §2), and nothing between reads the timer, so one Philox site
   // serves every handler of the wave (MR_TAPE builds record every draw: immediate there)
-#ifndef MR_RESET_ONCE
-#define MR_RESET_ONCE 1
-#endif
   uint32_t nrst = 0;
-#if MR_RESET_ONCE && !MR_TAPE
+#if !MR_TAPE
 #define RESET_ME() (nrst++)
 #else
 #define RESET_ME() reset_timer(D, x, me, d)
@@ -1613,14 +1266,14 @@ DI void node_event(const Dev& Darg, X& x, bool is_msg, uint32_t tnode, uint32_t 
     kind = type;
     if (!bit(x.alive, me) || !bit(x.conn, me) || !bit(x.conn, src) || link_cut(D, x, src, me)) {
       CADD(CNT_DROP_DELIVER, 1u);
-      nr_set(D, x, nr, 0, 16, me, seq, d);
+      rec_node(D, x, 0, 16, me, seq, d);
       PROF(P_DROP);
       return;
     }
     bool is_reply = (type == M_RV_REP || type == M_AE_REP || type == M_IS_REP);
     if (is_reply && inc != f_inc(d.f)) {
       CADD(CNT_DROP_STALE, 1u);
-      nr_set(D, x, nr, 0, 17, me, seq, d);
+      rec_node(D, x, 0, 17, me, seq, d);
       PROF(P_DROP);
       return;
     }
@@ -1629,7 +1282,7 @@ DI void node_event(const Dev& Darg, X& x, bool is_msg, uint32_t tnode, uint32_t 
         kv_request(D, x, me, d, src, inc, mterm, ma, mb, mc, prange_r);
         if (x.code != RUN) return;
         store_node(D, x, me, d);
-        nr_set(D, x, nr, 0, type, me, seq, d);
+        rec_node(D, x, 0, type, me, seq, d);
         return;
       }
     }
@@ -1706,40 +1359,17 @@ DI void node_event(const Dev& Darg, X& x, bool is_msg, uint32_t tnode, uint32_t 
         ae_load_batch(D, x, me, d, src, mat, pp, ma, k, j0, pe, lt, ov, ors);
         PROF(P_AE_PROBE);
         if (!(D.bugs & MR_F_BUG_NO_PREV_CHECK) && tp != pterm) {
-#ifndef MR_RUNSTART
-#define MR_RUNSTART 1
-#endif
-#if MR_RUNSTART  // fast backup: the run of term tp holding prev starts at rs(prev) (le_at)
           rb = prev <= d.snap ? prev : (rsp > d.snap + 1u ? rsp : d.snap + 1u);
-#else
-          uint32_t xx = prev;
-          while (xx - 1 > d.snap && term_at(D, x, me, d, xx - 1) == tp) xx--;
-          rb = xx;
-#endif
           break;
         }
         uint32_t tprev = tp, rsprev = rsp;  // the entry below the next one written
         bool wrote = false;
         CADD(CNT_SHIPPED, k - j0);  // the payload entries this receiver reads (zero-copy until here)
-        // MR_AE_COOP: the receiver walks the first batch; the entries after it go to the wave
-        const bool coop = MR_AE_COOP && !MR_TAPE && D.K <= AC + AE_COOP_REM;
+        // AE_COOP: the receiver walks the first batch; the entries after it go to the wave
+        const bool coop = AE_COOP && !MR_TAPE && D.K <= AC + AE_COOP_REM;
         const uint32_t jw = coop ? (k < j0 + AC ? k : j0 + AC) : k;
-#ifdef MR_DEV_AEDBG  // debug: lanes whose rest needs comparisons (MR_DEV_AEDBG 1) or all (2) walk it
-        for (uint32_t pass = 0; pass < 2; pass++) {
-        uint32_t kc = k;
-        if (pass == 1 && coop) {
-          const bool cmp = !wrote && d.last - ma > jw;
-          kc = (MR_DEV_AEDBG == 2 || cmp) ? jw : k;
-          if (!ae_recv_coop(D, x, me, d, src, mat, slot, ma, kc, jw, lrs, tprev, rsprev, wrote,
-                            prange_r.x, prange_r.y))
-            return;
-        }
-        const uint32_t ja = pass == 0 ? j0 : (coop && kc < k ? jw : k), jb = pass == 0 ? jw : k;
-        for (uint32_t j = ja; j < jb; j += AC) {
-#else
         for (uint32_t j = j0; j < jw; j += AC) {
-#endif
-          if (!MR_AE_PIPE && j != j0) ae_load_batch(D, x, me, d, src, mat, pp, ma, k, j, pe, lt, ov, ors);
+          if (j != j0) ae_load_batch(D, x, me, d, src, mat, pp, ma, k, j, pe, lt, ov, ors);
           if (D.safety) {  // MR_F_SAFETY log matching: same index and term => same entry
 #if !MR_AE_OWN
 #pragma unroll
@@ -1755,14 +1385,6 @@ DI void node_event(const Dev& Darg, X& x, bool is_msg, uint32_t tnode, uint32_t 
             }
             if (bad) { fail(D, x, MR_FAIL_SAFETY_LOG_MATCHING); return; }
           }
-          // MR_AE_PIPE: the next batch's loads issued before this batch's log writes, so they do
-          // not wait behind those stores (vmcnt retires in issue order). Safe: the next batch's
-          // indices are other ring slots, and its own-entry terms are only trusted below the
-          // current last (the skip test re-reads d.last, which a write can only lower to its index)
-          LE pe2[AC];
-          uint32_t lt2[AC], ors2[AC];
-          uint64_t ov2[AC];
-          if (MR_AE_PIPE && j + AC < jw) ae_load_batch(D, x, me, d, src, mat, pp, ma, k, j + AC, pe2, lt2, ov2, ors2);
 #pragma unroll
           for (uint32_t q = 0; q < AC; q++) {
             const uint32_t jx = j + q, i = ma + 1 + jx;
@@ -1773,11 +1395,7 @@ DI void node_event(const Dev& Darg, X& x, bool is_msg, uint32_t tnode, uint32_t 
               continue;
             }
             if (i - d.snap > D.log_cap) { fail(D, x, MR_FAIL_SIM_CAPACITY); return; }
-#if MR_PLO_EARLY
             guard_log_write(D, x, me, d.pexp, i, prange_r.x, prange_r.y);
-#else
-            guard_log_write(D, x, me, d.pexp, i);
-#endif
             rsprev = pe[q].term == tprev ? rsprev : i;
             tprev = pe[q].term;
             D.log[logi(D, x, me, i)] = LE{pe[q].term, rsprev, pe[q].val};
@@ -1787,18 +1405,10 @@ DI void node_event(const Dev& Darg, X& x, bool is_msg, uint32_t tnode, uint32_t 
             d.lastt = pe[q].term;
             CMAX(CNT_MAX_LOG, i - d.snap);
           }
-          if (MR_AE_PIPE && j + AC < jw) {
-#pragma unroll
-            for (uint32_t q = 0; q < AC; q++) { pe[q] = pe2[q]; lt[q] = lt2[q]; ov[q] = ov2[q]; ors[q] = ors2[q]; }
-          }
         }
-#ifdef MR_DEV_AEDBG
-        }
-#else
         if (coop && !ae_recv_coop(D, x, me, d, src, mat, slot, ma, k, jw, lrs, tprev, rsprev, wrote,
                                   prange_r.x, prange_r.y))
           return;
-#endif
         if (wrote) LRS(me) = rsprev;
         uint32_t lc = ma + k;
         if (mc < lc) lc = mc;
@@ -1876,33 +1486,25 @@ DI void node_event(const Dev& Darg, X& x, bool is_msg, uint32_t tnode, uint32_t 
   // clogs (net_send, SEMANTICS §4), so it needs only its accounting — a sequence number, a
   // send index, drop_clog — and none of the send path's loads (MR_TAPE builds record its
   // draw, so they send it the long way)
-#ifndef MR_CLOG_FAST
-#define MR_CLOG_FAST 1
-#endif
-  uint32_t reach = (MR_TAPE || !MR_CLOG_FAST) ? ~0u : (bit(x.conn, me) ? x.conn : 0u);
-  constexpr bool lean = MR_SEND_LEAN && !MR_TAPE && MR_CLOG_FAST;
+  uint32_t reach = MR_TAPE ? ~0u : (bit(x.conn, me) ? x.conn : 0u);
+  constexpr bool lean = !MR_TAPE;
   if (lean && D.links)  // links cut by disconnect2 / partition (link_cut): word me / 4, byte me % 4
     reach &= ~((CS(CS_CUT + (me >> 2)) >> (8u * (me & 3u))) & 0xFFu);
-#if MR_SEND_EARLY
   // a leader's appends read our terms at next[p] - 1: issue those loads before the applier's
   // checker stores (the ring slot is valid whatever the applier does; gated after it)
   uint32_t rawt[NB];
-#ifndef MR_RAWT_NEED  // only the terms the append will read (A/B round 4)
-#define MR_RAWT_NEED 1
-#endif
-  const uint32_t lbase0 = MR_RAWT_NEED ? sel_nb(pv.mt, me) : 0u;
+  const uint32_t lbase0 = sel_nb(pv.mt, me);
 #pragma unroll
   for (uint32_t p = 0; p < NB; p++) {
     const uint32_t ix = pv.nx[p] - 1u;
     // the append reads the ring only for an index below the leader's base that is neither the
     // snapshot nor the last entry (LPT below); the applier may raise the snapshot index, which
     // only turns a load into an InstallSnapshot or a snapshot-term read, never the other way
-    const bool need = !MR_RAWT_NEED || (ix != d.snap && ix != d.last && ix <= lbase0);
+    const bool need = ix != d.snap && ix != d.last && ix <= lbase0;
     rawt[p] = (mode == SEND_APPEND && bit(peers & reach, p) && p < D.n && ix != 0u && need)
                   ? D.log[logi(D, x, me, ix)].term : 0u;
   }
-#endif
-  if (MR_AP_COOP && !KV && kv_gen(S).maxraft == 0) {
+  if (!KV && kv_gen(S).maxraft == 0) {
     if (__ballot(d.applied < d.commit)) {  // committed entries reach the tester's applier
       node_apply_coop<S>(D, x, me, d);
       if (x.code != RUN) return;
@@ -1917,37 +1519,26 @@ DI void node_event(const Dev& Darg, X& x, bool is_msg, uint32_t tnode, uint32_t 
   const uint32_t lt = mode == SEND_VOTE ? d.lastt : 0u;  // term_at(last)
   // appends: next[p] of every peer, then the terms at next[p] - 1, as two
   // batches of independent loads, staged in LDS for the send loop
-  uint64_t snapv = 0;
   const uint32_t all = peers, seq0 = x.msgs_sent, ctr0 = d.nctr;
   peers &= reach;
   if (mode == SEND_APPEND) {  // only a leader appends
     uint32_t nxa[NB];
-    bool any_is = false;
     const uint32_t lbase = sel_nb(pv.mt, me);
 #pragma unroll
     for (uint32_t p = 0; p < NB; p++) {
       nxa[p] = bit(peers, p) ? pv.nx[p] : 0u;
-      any_is |= bit(peers, p) && nxa[p] <= d.snap;
     }
 #pragma unroll
     for (uint32_t p = 0; p < NB; p++) {  // term_at(next[p] - 1)
       const uint32_t pv = nxa[p] - 1u;
       const bool ld = bit(peers, p) && nxa[p] > d.snap && pv != 0u && pv != d.snap &&
                       pv != d.last && pv <= lbase;
-#if MR_SEND_EARLY
       const uint32_t t = ld ? rawt[p] : 0u;
-#else
-      const uint32_t t = ld ? D.log[logi(D, x, me, pv)].term : 0u;
-#endif
       LNX(p) = nxa[p];
       LPT(p) = pv == 0u ? 0u : pv == d.snap ? d.snapt : pv == d.last ? d.lastt : pv > lbase ? d.term : t;
     }
-    if (!MR_WAIT_HYGIENE && any_is) snapv = NSV(me);
   }
   uint32_t plo_acc = ~0u, phi_acc = 0u;  // index range referenced by this event's payloads
-#ifndef MR_SEND_HOIST  // the fields every send of the event shares, chosen once before the loop
-#define MR_SEND_HOIST 1
-#endif
   // a reply or a vote request carries the same fields to every peer; an append's come from
   // the peer's next[] (LDS staging) inside the loop
   const bool rep = mode == SEND_REPLY;
@@ -1961,18 +1552,12 @@ DI void node_event(const Dev& Darg, X& x, bool is_msg, uint32_t tnode, uint32_t 
     const uint32_t below = all & ((1u << p) - 1u);  // earlier sends of this event, clogged ones too
     x.msgs_sent = seq0 + (uint32_t)__builtin_popcount(below);
     d.nctr = ctr0 + (uint32_t)__builtin_popcount(below);
-    uint32_t st, sa, sb, sc, sk = 0, prev = 0;
+    uint32_t st = st0, sa = sa0, sb = sb0, sc = sc0, sk = 0, prev = 0;
     uint64_t sv = 0;
-    if (MR_SEND_HOIST) {
-      st = st0; sa = sa0; sb = sb0; sc = sc0;
-    } else {
-      st = M_RV_REQ; sa = me; sb = d.last; sc = lt;
-      if (mode == SEND_REPLY) { st = rtype; sa = ra; sb = rb; sc = 0; }
-    }
     if (mode == SEND_APPEND) {
       const uint32_t nx = LNX(p);
       if (has_snaps(S) && nx <= d.snap) {
-        st = M_IS_REQ; sa = d.snap; sb = d.snapt; sc = 0; sv = MR_WAIT_HYGIENE ? NSV(me) : snapv;
+        st = M_IS_REQ; sa = d.snap; sb = d.snapt; sc = 0; sv = NSV(me);
       } else {
         prev = nx - 1;
         sk = d.last - prev;
@@ -1995,7 +1580,7 @@ DI void node_event(const Dev& Darg, X& x, bool is_msg, uint32_t tnode, uint32_t 
     }
   }
   if (sfail) {
-    if (lean && !MR_FAIL_DEFER) rec_simple(D, x, 3, x.code);  // the verdict net_send left unrecorded
+    if (lean) rec_simple(D, x, 3, x.code);  // the verdict net_send left unrecorded
     CADD(CNT_DROP_CLOG, sclog);
     return;
   }
@@ -2011,7 +1596,7 @@ DI void node_event(const Dev& Darg, X& x, bool is_msg, uint32_t tnode, uint32_t 
   }
   PROF(P_SEND);
   store_node(D, x, me, d);
-  nr_set(D, x, nr, is_msg ? 0u : 1u, kind, me, is_msg ? seq : 0u, d);
+  rec_node(D, x, is_msg ? 0u : 1u, kind, me, is_msg ? seq : 0u, d);
   PROF(P_STORE);
 }
 
@@ -2047,19 +1632,9 @@ DI void t_new(const Dev& D, X& x, bool snapshot) {  // RaftTester::new, tester.r
   for (uint32_t i = 0; i < D.n; i++) { t_start1(D, x, i); t_conn(D, x, i, 1); }
   if (D.unrel_flag) t_set_unrel(x, true);
 }
-// bit mask of the servers whose role is leader: one batch of independent loads
-// (a start() changes only its own server, so a loop of starts can use it)
-#ifndef MR_LMASK
-#define MR_LMASK 1
-#endif
-DI uint32_t t_leaders(const Dev& D, X& x) {
-  if (MR_LMASK) return x.lmask;
-  uint32_t m = 0;
-#pragma unroll
-  for (uint32_t i = 0; i < NB; i++)
-    m |= (i < D.n && f_role(ND(NF_FLAGS, i)) == R_L) ? 1u << i : 0u;
-  return m;
-}
+// bit mask of the servers whose role is leader: x.lmask, kept by store_node (every role change
+// of a record passes there), so is_leader() sampling reads no record
+DI uint32_t t_leaders(const Dev& D, X& x) { return x.lmask; }
 // tester.rs:165-171 -> raft.rs:238-244; unwrap() on a crashed raft panics.
 // `lead` = whether server i is leader (t_leaders), read before the call.
 DI bool t_start(const Dev& D, X& x, uint32_t i, uint64_t v, uint32_t& idx, uint32_t& term,
@@ -2141,10 +1716,7 @@ DI uint32_t t_term(const Dev& D, X& x, uint32_t i) {
 }
 // The tester's checks over every server read each record's words as one batch of loads
 // (unrolled over the node bound): a loop that loads server by server is one round trip per
-// server, and one per server index some lane needs (MR_T_BATCH; A/B in DESIGN.md §6.8)
-#ifndef MR_T_BATCH
-#define MR_T_BATCH 1
-#endif
+// server, and one per server index some lane needs (A/B in DESIGN.md §6.8)
 // the terms of every server (words NF_TERM), 0 past D.n
 DI void t_terms(const Dev& D, X& x, uint32_t (&tm)[NB]) {
 #pragma unroll
@@ -2152,37 +1724,29 @@ DI void t_terms(const Dev& D, X& x, uint32_t (&tm)[NB]) {
 }
 DI uint32_t t_log_size(const Dev& D, X& x) {  // tester.rs:152-158 + SEMANTICS §5 size model
   uint32_t mx = 0;
-  if (MR_T_BATCH) {
-    uint32_t fl[NB], la[NB], sn[NB];
+  uint32_t fl[NB], la[NB], sn[NB];
 #pragma unroll
-    for (uint32_t q = 0; q < NB; q++) {
-      const bool in = q < D.n;
-      fl[q] = in ? ND(NF_FLAGS, q) : 0u;
-      la[q] = in ? ND(NF_LAST, q) : 0u;
-      sn[q] = in ? ND(NF_SNAP, q) : 0u;
-    }
-#pragma unroll
-    for (uint32_t q = 0; q < NB; q++) {
-      const uint32_t sz = 32u + (f_voted(fl[q]) != 15u ? 9u : 1u) + 24u * (la[q] - sn[q]);
-      if (q < D.n && sz > mx) mx = sz;
-    }
-    return mx;
+  for (uint32_t q = 0; q < NB; q++) {
+    const bool in = q < D.n;
+    fl[q] = in ? ND(NF_FLAGS, q) : 0u;
+    la[q] = in ? ND(NF_LAST, q) : 0u;
+    sn[q] = in ? ND(NF_SNAP, q) : 0u;
   }
-  for (uint32_t i = 0; i < D.n; i++) {
-    uint32_t sz = 32u + (f_voted(ND(NF_FLAGS, i)) != 15u ? 9u : 1u) +
-                  24u * (ND(NF_LAST, i) - ND(NF_SNAP, i));
-    if (sz > mx) mx = sz;
+#pragma unroll
+  for (uint32_t q = 0; q < NB; q++) {
+    const uint32_t sz = 32u + (f_voted(fl[q]) != 15u ? 9u : 1u) + 24u * (la[q] - sn[q]);
+    if (q < D.n && sz > mx) mx = sz;
   }
   return mx;
 }
 DI uint32_t t_check_terms(const Dev& D, X& x) {  // tester.rs:95-109
   uint32_t term = 0;
   uint32_t tm[NB];
-  if (MR_T_BATCH) t_terms(D, x, tm);
+  t_terms(D, x, tm);
   for (uint32_t i = 0; i < D.n; i++) {
     if (!bit(x.conn, i)) continue;
     if (!bit(x.alive, i)) { fail(D, x, MR_FAIL_UNWRAP_NONE); return 0; }
-    uint32_t xt = MR_T_BATCH ? sel_nb(tm, i) : ND(NF_TERM, i);
+    uint32_t xt = sel_nb(tm, i);
     if (term == 0) term = xt;
     else if (term != xt) { fail(D, x, MR_FAIL_TERM_DISAGREE); return 0; }
   }
@@ -2208,19 +1772,13 @@ DI void t_end(const Dev& D, X& x) {  // tester.rs:339-358
 DI uint32_t nd_role(const Dev& D, X& x, uint32_t i) { return f_role(ND(NF_FLAGS, i)); }
 DI uint32_t nd_term(const Dev& D, X& x, uint32_t i) { return ND(NF_TERM, i); }
 #define TV(k) C64(C64_TV + (k))
-#ifndef MR_T_LAUNDER  // A/B: the tester (body and threads) on the laundered argument copy
-#define MR_T_LAUNDER 0
-#endif
 #include "mr_tester.inc"
 
 // one tester event: resume the cluster's coroutine until it sleeps or ends
 template <uint32_t S>
 DI void tester(const Dev& Darg, X& x) {
-  const Dev D = MR_T_LAUNDER ? dev_launder<S>(Darg) : Darg;
+  const Dev& D = Darg;
   T t;
-#ifdef MR_DEV_PRIO
-  __builtin_amdgcn_s_setprio(MR_DEV_PRIO);
-#endif
   // the frame: one cluster-major 80-B record (mr_dev.h TF_Q), five 16-B loads from one address
   // instead of 17 cluster-minor words with 17 field bases (which the compiler keeps live in
   // scalar registers across the step loop)
@@ -2234,9 +1792,6 @@ DI void tester(const Dev& Darg, X& x) {
   t.h[0] = q2.z; t.h[1] = q2.w; t.h[2] = q3.x; t.h[3] = q3.y; t.h[4] = q3.z;
   t.hv = ((uint64_t)q4.x << 32) | q3.w;
   static_assert(T_NL == 8 && T_NH == 5, "tester frame record layout");
-#ifdef MR_DEV_PRIO
-  __builtin_amdgcn_s_setprio(0);
-#endif
   x.yield = 0;
   for (int guard = 0;; guard++) {
     if (guard > 4096) { fail(D, x, MR_FAIL_SIM_BAD_PROGRAM); return; }
@@ -2245,11 +1800,11 @@ DI void tester(const Dev& Darg, X& x) {
       if constexpr (is_svc(S)) {
         done = t.helper == H_CALL ? call_step(D, x, t) : join_step(D, x, t);
       } else if constexpr (nthr(S) > 0) {
-        done = t.helper == H_ONE    ? one_step(D, x, t, true)
+        done = t.helper == H_ONE    ? one_step(D, x, t)
                : t.helper == H_WAIT ? wait_step(D, x, t)
                                     : join_step(D, x, t);  // H_JOIN: join_all
       } else {
-        done = t.helper == H_ONE   ? one_step(D, x, t, true)
+        done = t.helper == H_ONE   ? one_step(D, x, t)
                : t.helper == H_COL ? col_step(D, x, t)
                                    : wait_step(D, x, t);
       }
@@ -2279,9 +1834,6 @@ DI void tester(const Dev& Darg, X& x) {
 // ---------------------------------------------------------------- kernels
 constexpr uint32_t CLS_MSG = 0, CLS_TIMER = 1, CLS_TESTER = 2, CLS_NONE = 3;
 
-#ifndef MR_WAVES_PER_EU
-#define MR_WAVES_PER_EU 2
-#endif
 // a cluster's run state into the lane (registers, LDS message keys) and back: at the start and
 // end of a launch, and when a lane that finished its cluster takes the next one (D.stream)
 template <uint32_t S>
@@ -2298,10 +1850,8 @@ DI void lane_load(const Dev& D, X& x) {
 #pragma unroll
   for (uint32_t w = 0; w < MW; w++) x.free_mask[w] = C64(w ? C64_FREE1 + w - 1 : C64_FREE);
   x.digest = C64(C64_DIGEST); x.mmin = C64(C64_MMIN);
-#if !MR_CNT_MEM
 #pragma unroll
   for (uint32_t k = 0; k < CNT__N; k++) x.cnt[k] = CS(CS_CNT + k);
-#endif
   for (uint32_t s = 0; s < D.M; s++) LK(s) = (lkey_t)MKEY(s);
   // every load above completes here (each loaded register is read by an empty asm): a lane that
   // takes a new cluster inside the step loop (streaming) then leaves no load pending into the
@@ -2316,10 +1866,8 @@ DI void lane_load(const Dev& D, X& x) {
   for (uint32_t d = 0; d < NB; d++) asm volatile("" ::"v"(x.timer[d]));
 #pragma unroll
   for (uint32_t w = 0; w < MW; w++) asm volatile("" ::"v"(x.free_mask[w]));
-#if !MR_CNT_MEM
 #pragma unroll
   for (uint32_t k = 0; k < CNT__N; k++) asm volatile("" ::"v"(x.cnt[k]));
-#endif
 }
 template <uint32_t S>
 DI void lane_store(const Dev& D, X& x) {
@@ -2336,10 +1884,8 @@ DI void lane_store(const Dev& D, X& x) {
 #pragma unroll
   for (uint32_t w = 0; w < MW; w++) C64(w ? C64_FREE1 + w - 1 : C64_FREE) = x.free_mask[w];
   C64(C64_DIGEST) = x.digest; C64(C64_MMIN) = x.mmin;
-#if !MR_CNT_MEM
 #pragma unroll
   for (uint32_t k = 0; k < CNT__N; k++) CS(CS_CNT + k) = x.cnt[k];
-#endif
   if (x.code != RUN) return;  // a finished cluster's messages are never read again
   for (uint32_t s = 0; s < D.M; s++) MKEY(s) = LK(s) == LKEY_FREE ? ~0ull : (uint64_t)LK(s);
 }
@@ -2371,25 +1917,19 @@ DI bool lane_claim(const Dev& D, X& x, bool want) {
 // waves per SIMD the register allocation targets: the kvraft / shard_ctrler kernels keep 64
 // message slots (LDS for one wave per SIMD), so they take the whole register file and keep
 // their overflow in AGPRs instead of scratch (config 5: 299 -> 265 ms)
+// (and the generic 8-server instances, which serve only node counts without an exact one: one
+// wave per SIMD, no scratch); the other kernels two waves per SIMD
 template <uint32_t S>
-#ifndef MR_SVC_WAVES
-#define MR_SVC_WAVES 1
-#endif
-#ifndef MR_NB8_WAVES  // the generic 8-server instances (any node count without an exact one)
-#define MR_NB8_WAVES 1
-#endif
 constexpr uint32_t step_waves() {
-  return NB >= 8 ? (uint32_t)MR_NB8_WAVES : is_svc(S) ? (uint32_t)MR_SVC_WAVES : (uint32_t)MR_WAVES_PER_EU;
+  return NB >= 8 || is_svc(S) ? 1u : 2u;
 }
 // exact-size instances (NB < 8, mr_dev.h has_exact): the node count is NB at compile time
-#ifndef MR_EXACT_N
-#define MR_EXACT_N (MR_NB < MR_MAX_NODES)
-#endif
+constexpr bool EXACT_N = MR_NB < MR_MAX_NODES;
 template <uint32_t S, uint32_t NBT>
 __global__ void __launch_bounds__(STEP_BLOCK, step_waves<S>()) step_kernel(Dev Din, uint32_t budget) {
   static_assert(NBT == NB, "one node bound per translation unit");
   Dev D = Din;
-  if constexpr (MR_EXACT_N) D.n = NB;  // the host launches this instance for D.n == NB only
+  if constexpr (EXACT_N) D.n = NB;  // the host launches this instance for D.n == NB only
   // configuration the scenario fixes (mr_host.cpp sets the same values): compile-time here, so no
   // loop-invariant predicate on them is kept in scalar registers across the step loop
   D.nthr = nthr(S);
@@ -2399,19 +1939,6 @@ __global__ void __launch_bounds__(STEP_BLOCK, step_waves<S>()) step_kernel(Dev D
   if constexpr (kv_gen(S).maxraft == 0) D.kvs32 = nullptr;
   if constexpr (is_svc(S)) __builtin_assume(D.kv32 != nullptr);
   if constexpr (kv_gen(S).maxraft > 0) __builtin_assume(D.kvs32 != nullptr);
-#ifdef MR_DEV_LEAN  // A/B: test-only features compiled out (bug variants, streaming, traces, null Raft)
-  D.bugs = 0; D.stream = 0; D.trace_clusters = 0; D.null_raft = 0;
-  if constexpr (!is_kv(S)) D.links = 0;
-#endif
-#ifdef MR_DEV_NOSTREAM
-  D.stream = 0;
-#endif
-#ifdef MR_DEV_NOBUGS
-  D.bugs = 0;
-#endif
-#ifdef MR_DEV_NOTRACE
-  D.trace_clusters = 0;
-#endif
   X x;
   // lanes 0 .. lpw - 1 of each 64-lane block hold clusters (D.lpw < 64: a batch smaller than the
   // resident lanes still spreads over two waves per SIMD; the other lanes idle)
@@ -2472,58 +1999,33 @@ __global__ void __launch_bounds__(STEP_BLOCK, step_waves<S>()) step_kernel(Dev D
     const uint32_t nm = __popcll(__ballot(run && cls == CLS_MSG));
     const uint32_t nt = __popcll(__ballot(run && cls == CLS_TIMER));
     const uint32_t ns = __popcll(__ballot(run && cls == CLS_TESTER));
-#ifndef MR_TESTER_NUM  // tester events run when >= NUM/DEN of the live lanes want them
-#define MR_TESTER_NUM 1
-#define MR_TESTER_DEN 3
-#endif
-#ifndef MR_MERGE_NODE  // message and timer events share one class (one node_event pass)
-#define MR_MERGE_NODE 1
-#endif
-    const bool tpick = MR_TESTER_DEN * ns >= MR_TESTER_NUM * (nm + nt + ns);
-    const uint32_t pick = tpick ? CLS_TESTER : (nm >= nt ? CLS_MSG : CLS_TIMER);
-#ifdef MR_ALL_CLASSES  // experiment: every lane runs its own event (divergent paths)
-    bool mine = true;
-#else
-    bool mine = MR_MERGE_NODE ? (tpick ? cls == CLS_TESTER : cls != CLS_TESTER) : cls == pick;
-#endif
+    // tester events run when >= 1/3 of the live lanes want them (A/B: 1/4, 2/5, 1/2 lose
+    // 0.3-2.6 %), node events (messages and timers, one node_event pass) otherwise
+    const bool tpick = 3u * ns >= nm + nt + ns;
+    bool mine = tpick ? cls == CLS_TESTER : cls != CLS_TESTER;
     // AppendEntries deliveries (the longest node path: probe, payload batches, log writes) wait
     // until they are >= AE_NUM / AE_DEN of the wave's node events, so the other node events run
     // without their round trips; like any lane that waits, a cluster's own order is unchanged
-#ifndef MR_AE_ALL  // A/B: the AppendEntries sub-class for every 64-bit-key scenario
-#define MR_AE_ALL 0
-#endif
-    if constexpr (MR_AE_CLASS && !MR_KEY32 && (MR_AE_ALL || (!is_svc(S) && !restarts_servers(S)))) {
+    if constexpr (!MR_KEY32 && !is_svc(S) && !restarts_servers(S)) {
       if (!tpick) {
         const bool ae = run && cls == CLS_MSG && ((key >> 5) & 1u);
         const uint32_t nae = __popcll(__ballot(ae));
-        if (nae < nm + nt && MR_AE_DEN * nae < MR_AE_NUM * (nm + nt) &&
-            nm + nt - nae >= MR_AE_OTHERS)
-          mine = mine && !ae;
-        if constexpr (MR_HB_CLASS) {
-          const bool hb = run && cls == CLS_TIMER && bit(x.lmask, node);
-          const uint32_t nhb = __popcll(__ballot(hb));
-          if (nhb < nm + nt && MR_AE_DEN * nhb < MR_AE_NUM * (nm + nt)) mine = mine && !hb;
-        }
+        if (nae < nm + nt && 2u * nae < nm + nt && nm + nt - nae >= AE_OTHERS) mine = mine && !ae;
       }
     }
     PROF(P_SEL);
     if (!run || !mine) continue;
     if (nthr(S) > 0 && (uint32_t)(key >> 32) == INF_T) {  // nothing can wake the test body
       fail(D, x, MR_FAIL_SIM_BAD_PROGRAM);
-      fail_flush(D, x);
       continue;
     }
     x.now = (uint32_t)(key >> 32);
     need = true;
     x.events++;
-    if (x.events > D.max_events) { fail(D, x, MR_FAIL_SIM_EVENT_LIMIT); fail_flush(D, x); continue; }
+    if (x.events > D.max_events) { fail(D, x, MR_FAIL_SIM_EVENT_LIMIT); continue; }
     if (cls != CLS_TESTER) {
       CADD(cls == CLS_MSG ? CNT_EV_MSG : CNT_EV_TIMER, 1u);
-      NR nr;
-      nr.on = false;
-      node_event<S>(D, x, cls == CLS_MSG, node, x.mslot, ((uint32_t)key & 0x3FFFFFFFu) >> 6, nr);
-      if (MR_REC_ONCE && nr.on && x.code == RUN)
-        rec8(D, x, x.now, nr.w1, nr.aux, nr.term, nr.commit, nr.applied, nr.last, nr.snap);
+      node_event<S>(D, x, cls == CLS_MSG, node, x.mslot, ((uint32_t)key & 0x3FFFFFFFu) >> 6);
     } else {
       CADD(CNT_EV_TESTER, 1u);
       if constexpr (nthr(S) > 0) {
@@ -2534,7 +2036,6 @@ __global__ void __launch_bounds__(STEP_BLOCK, step_waves<S>()) step_kernel(Dev D
       }
       PROF(P_TESTER);
     }
-    fail_flush(D, x);
   }
 #ifdef MR_PROF
   PROF(P_TAIL);

@@ -120,6 +120,21 @@ def test_cli_net_mode_defaults_to_the_tests_own():
     assert trace.events_from_decisions(rel, unreliable=False)[0]["latency_us"] == 9000
 
 
+@pytest.mark.parametrize("test", ["unreliable_agree_2c", "unreliable_churn_2c"])
+def test_cli_net_mode_rejects_mixed_mode_logs(test):
+    """tests that switch the net back to reliable part-way (tests.rs:680, :832) have
+    no single mode, so a send line without its own "unreliable" field is rejected, not decoded
+    under the unreliable latency range; lines that carry it, and --unreliable runs, still load."""
+    from madraft_amd.__main__ import net_mode
+    assert net_mode(test, False) is None
+    assert net_mode(test, True) is True
+    line = {"event": "send", "host": 0, "index": 0, "latency_us": 9000}
+    with pytest.raises(ValueError):
+        trace.decisions_from_events([line], unreliable=net_mode(test, False))
+    d = trace.decisions_from_events([dict(line, unreliable=False)], unreliable=net_mode(test, False))
+    assert trace.events_from_decisions(d, unreliable=False)[0]["latency_us"] == 9000
+
+
 @pytest.mark.gpu
 def test_gpu_replays_an_imported_event_log(hip, oracle, tmp_path):
     cfg = oracle.cfg("figure_8_unreliable_2c", iters=100)
