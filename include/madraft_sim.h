@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define MR_ABI_VERSION 3u
+#define MR_ABI_VERSION 4u
 #define MR_MAX_NODES 8u
 #define MR_MAX_MSG_SLOTS 256u
 #define MR_MAX_AE 32u
@@ -137,6 +137,10 @@ static inline uint32_t mr_kv_log_cap(uint32_t s) {
 #define MR_F_BUG_STALE_READ 0x200u /* a leader answers Get from its local state, not via the log */
 #define MR_F_STREAM 0x400u   /* with lanes < n_clusters: a lane whose cluster has its verdict takes
                               * the next unstarted cluster (default: chunks of `lanes` clusters) */
+/* Test-only (ABI 4): the tester's apply checker records values but does not compare them
+ * (tester.rs:384-388 disabled), so a diverging Raft runs on and the traces' apply digests
+ * (mr_trace_digests) are what must catch it */
+#define MR_F_BUG_NO_APPLY_CHECK 0x800u
 
 /* ---- verdicts: one code per tester panic site ---- */
 enum mr_fail {
@@ -267,6 +271,9 @@ typedef struct mr_counters {
   uint64_t entries_materialized; /* zero-copy payload entries copied before their log slot was
                                   * overwritten (HIP path only; the oracle copies at send) */
   uint64_t kv_lin_checked;  /* Get results the linearizability checker verified (SEMANTICS §9a) */
+  /* ABI 4 */
+  uint64_t coop_entries;    /* HIP path only: AppendEntries entries a receiver's wave wrote for it
+                             * (the cooperative receive of the 7- / 8-server step kernels) */
 } mr_counters;
 
 typedef struct mr_run_stats {
@@ -317,6 +324,30 @@ int mr_batch_verdicts(mr_batch* b, uint16_t* code, uint32_t* time_us, uint64_t* 
 int mr_batch_counters(mr_batch* b, mr_counters* out);
 /* Trace of traced cluster `k` (k < trace_clusters). *n = records written. */
 int mr_trace_get(mr_batch* b, uint32_t k, mr_event* out, size_t cap, size_t* n);
+/* ABI 4: the apply-digest term of log entry i with command value v (splitmix64's finalizer of
+ * v ^ i * golden ratio); the kernels compute the same in device code */
+static inline uint64_t mr_apply_mix(uint32_t i, uint64_t v) {
+  uint64_t z = v ^ ((uint64_t)i * 0x9E3779B97F4A7C15ull);
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+/* ABI 4: the apply digest of each of those records (docs/SEMANTICS.md §7): for a node event,
+ * the sum mod 2^64 of mr_apply_mix(i, value_i) over the entries i = 1..applied the node applied
+ * one by one; UINT64_MAX once it installed a snapshot or restarted above index 0; 0 for other
+ * records. Equal applied indices with different digests = state-machine safety broken by
+ * value, checkable from the trace alone (tests/test_trace_properties.py). */
+int mr_trace_digests(mr_batch* b, uint32_t k, uint64_t* out, size_t cap, size_t* n);
+/* ABI 4: the key-value commands of traced cluster k as the service applied them (kvraft
+ * scenarios; zero rows elsewhere): out[2 i] = log entry i's command (SEMANTICS §9 layout), out[2 i
+ * + 1] = the hash of its key's value right after the first server to apply entry i applied it
+ * (a Get: the hash it answers). Rows i < min(cap, trace_cap); *n = 1 + the highest index
+ * recorded. The log by value and the servers' state machine, checkable against a replay of
+ * the real strings (tests/test_kv_trace.py). */
+int mr_trace_applies(mr_batch* b, uint32_t k, uint64_t* out, size_t cap, size_t* n);
+/* ABI 4: the kernel the batch's launches run: "pool_kernel", "step_kernel" or
+ * "step_kernel_tape" (keyed decisions set or recorded) */
+const char* mr_batch_kernel(const mr_batch* b);
 void mr_batch_destroy(mr_batch* b);
 
 /* ---- keyed decision traces and replay (docs/SEMANTICS.md §12) ----

@@ -7,7 +7,7 @@ import ctypes as C
 
 import numpy as np
 
-MR_ABI_VERSION = 3
+MR_ABI_VERSION = 4
 MR_MAX_NODES = 8
 MR_RUNNING = 0xFFFF
 MR_PASS = 0
@@ -23,6 +23,17 @@ MR_F_RECORD = 0x80
 MR_F_BUG_NO_DEDUP = 0x100
 MR_F_BUG_STALE_READ = 0x200
 MR_F_STREAM = 0x400  # lanes < clusters: finished lanes take the next cluster (mr_cfg.lanes)
+MR_F_BUG_NO_APPLY_CHECK = 0x800  # test-only: apply checker compares no values (ABI 4)
+DIGEST_INVALID = (1 << 64) - 1  # mr_trace_digests: the node's prefix was not applied entry by entry
+
+
+def apply_mix(i, v):
+    """include/madraft_sim.h mr_apply_mix: the apply-digest term of entry i with value v."""
+    m = (1 << 64) - 1
+    z = (v ^ (i * 0x9E3779B97F4A7C15)) & m
+    z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & m
+    z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & m
+    return z ^ (z >> 31)
 
 README_SEED = 1629626496  # /root/reference/README.md:48
 
@@ -105,7 +116,8 @@ class MrCounters(C.Structure):
                                ("cov_events", C.c_uint64 * 16), ("kv_ops", C.c_uint64),
                                ("kv_checked", C.c_uint64), ("log_writes", C.c_uint64),
                                ("entries_materialized", C.c_uint64),
-                               ("kv_lin_checked", C.c_uint64)]
+                               ("kv_lin_checked", C.c_uint64),
+                               ("coop_entries", C.c_uint64)]  # ABI 4
 
     def to_dict(self):
         d = {n: getattr(self, n) for n, _ in self._fields_
@@ -159,4 +171,5 @@ EXPORTS = [
     "mr_cfg_init", "mr_batch_create", "mr_batch_reset", "mr_batch_run", "mr_batch_verdicts",
     "mr_batch_counters", "mr_trace_get", "mr_batch_destroy", "mr_batch_set_decisions",
     "mr_batch_get_decisions", "mr_decision_word", "mr_replay", "mr_batch_submit", "mr_batch_finish",
+    "mr_trace_digests", "mr_trace_applies", "mr_batch_kernel",  # ABI 4
 ]

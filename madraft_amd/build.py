@@ -12,6 +12,11 @@ import subprocess
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 LIB = os.path.join(HERE, "lib", "libmadraft_hip.so")
+# the MR_GUARD debug library (mr_kernel.hip GI: every computed per-cluster index checked): the
+# instances that use scratch or faulted once — count_2b, the churn tests (round 3's 8-server
+# fault was step_kernel<18, 8>), every kvraft / shard_ctrler test — and the headline
+GUARD_LIB = os.path.join(HERE, "lib", "libmadraft_guard.so")
+GUARD_SCNS = [10, 16, 17, 18] + list(range(25, 48))
 ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950")
 
 
@@ -52,7 +57,7 @@ def has_pool(i, nb):
     return nb <= 5 and has_exact(i, nb) and i in POOL_SCNS
 
 
-def _units(csrc, scns=None):
+def _units(csrc, scns=None, tape=True):
     kern = os.path.join(csrc, "mr_kernel.hip")
     units = [(kern, "common", ["-DMR_COMMON=1", "-DMR_SCN_LIST=", "-DMR_NB=8"])]
     for nb in (3, 5, 7, 8):
@@ -79,7 +84,7 @@ def _units(csrc, scns=None):
             lst = " ".join(f"MR_INST({i})" for i in ids[g::ng])
             units.append((kern, f"pool{nb}_{g}", ["-DMR_COMMON=0", f"-DMR_SCN_LIST={lst}",
                                                   f"-DMR_NB={nb}", "-DMR_KEY32=1", "-DMR_POOL=1"]))
-    ids = list(scns or SCN_IDS)  # decision-tape builds (SEMANTICS §12), NB = 8
+    ids = list(scns or SCN_IDS) if tape else []  # decision-tape builds (SEMANTICS §12), NB = 8
     wide = [i for i in ids if i in WIDE_SLOTS]
     ids = [i for i in ids if i not in WIDE_SLOTS]
     ng = max(1, min(N_GROUPS, (len(ids) + 3) // 4)) if ids else 0
@@ -97,16 +102,16 @@ def _units(csrc, scns=None):
     return units
 
 
-def build_hip(force=False, verbose=False, extra=(), out=None, scns=None, csrc=None):
+def build_hip(force=False, verbose=False, extra=(), out=None, scns=None, csrc=None, tape=True):
     """Compile the product library; `extra` flags / `out` path / only scenario ids `scns` /
-    another source tree `csrc` (a snapshot laid out as madraft_amd/csrc + include/) for dev
-    variants."""
+    another source tree `csrc` (a snapshot laid out as madraft_amd/csrc + include/) / no
+    decision-tape kernels (`tape`) for dev variants."""
     out = out or LIB
     csrc = csrc or os.path.join(HERE, "csrc")
     srcs = sorted(glob.glob(os.path.join(csrc, "*.hip")) + glob.glob(os.path.join(csrc, "*.cpp")))
     deps = srcs + glob.glob(os.path.join(csrc, "*.h")) + glob.glob(os.path.join(csrc, "*.inc")) + \
         [os.path.join(ROOT, "include", "madraft_sim.h"), os.path.abspath(__file__)]
-    if not force and not extra and not _stale(out, deps):
+    if not force and not _stale(out, deps):
         return out
     objdir = os.path.join(HERE, "lib", "obj" + ("_" + os.path.basename(out) if out != LIB else ""))
     os.makedirs(objdir, exist_ok=True)
@@ -114,7 +119,7 @@ def build_hip(force=False, verbose=False, extra=(), out=None, scns=None, csrc=No
             "-Wno-unused-function", *extra]
     jobs, objs, running = [], [], []
     njobs = max(1, min(16, os.cpu_count() or 1))
-    for src, name, flags in _units(csrc, scns):
+    for src, name, flags in _units(csrc, scns, tape):
         obj = os.path.join(objdir, name + ".o")
         objs.append(obj)
         cmd = base + flags + ["-c", src, "-o", obj]
@@ -137,6 +142,12 @@ def build_hip(force=False, verbose=False, extra=(), out=None, scns=None, csrc=No
     subprocess.run(cmd, check=True)
     os.replace(out + ".tmp", out)
     return out
+
+
+def build_guard(force=False, verbose=False):
+    """The MR_GUARD library (tests/test_guard.py), without decision-tape kernels."""
+    return build_hip(force=force, verbose=verbose, extra=["-DMR_GUARD=1"], out=GUARD_LIB,
+                     scns=GUARD_SCNS, tape=False)
 
 
 def build_oracle(verbose=False):

@@ -31,7 +31,7 @@ enum : uint32_t { ST_TESTER = 1, ST_ELECT = 2, ST_NET = 3 };
 enum : uint32_t {
   CNT_EV_MSG, CNT_EV_TIMER, CNT_EV_TESTER, CNT_DROP_CLOG, CNT_DROP_LOSS, CNT_DROP_OVERFLOW,
   CNT_DROP_DELIVER, CNT_DROP_STALE, CNT_ELECTIONS, CNT_LEADERS, CNT_APPLIES, CNT_SNAPSHOTS,
-  CNT_INSTALLS, CNT_SHIPPED, CNT_LOG_WRITES, CNT_MATERIALIZED,
+  CNT_INSTALLS, CNT_SHIPPED, CNT_LOG_WRITES, CNT_MATERIALIZED, CNT_COOP,
   CNT_MAX_INFLIGHT, CNT_MAX_LOG, CNT_MAX_INDEX, CNT__N
 };
 
@@ -198,6 +198,9 @@ struct Dev {
   uint32_t* op32;   // [C][OP_CAP][OPW]       shard_ctrler operations
   uint32_t nthr;    // thread slots of kt32 (0 = none)
   mr_event* trace;  // [trace_clusters][trace_cap]
+  uint64_t* tdig;   // [trace_clusters][trace_cap] apply digest of each record (ABI 4)
+  uint64_t* tapp;   // [trace_clusters][trace_cap][2] KV command, key hash after it (ABI 4)
+  uint64_t* adig;   // [trace_clusters][MR_MAX_NODES][2] per node: digest sum, invalid flag
   uint32_t* led;    // [C][LED_W] MR_F_SAFETY: bit t = a leader was elected in term t
   uint32_t* lin32;  // [C][KV_KEYS][KV_APP][LINW] kvraft linearizability bookkeeping (§9a, §9b)
   uint32_t lin15;   // generic_test_linearizability layout (§9b): key records / bookkeeping
@@ -214,6 +217,7 @@ struct Dev {
   uint4* tfr;       // [C][TF_Q] the tester coroutine frame, one cluster-major 80-B record
   uint32_t* kwk;    // [C][kws(nthr)][2] thread slots' {tid, wake}: the scheduler's keys, packed
   uint32_t pool;    // the batch runs on pool_kernel (has_pool): 32-bit keys with the AE bit
+  uint32_t* guard;  // [4] MR_GUARD builds: an out-of-range index {tag, cluster, index, bound}
 };
 // words-pairs per cluster of kwk: the thread slots rounded up to whole 16-B quads (two slots each;
 // slot 0 = the test body and the pad slot hold ~0, so they never win a rescan)

@@ -309,7 +309,7 @@ static int mr_batch_create_impl(const mr_cfg* cfg, mr_batch** out) {
   D.unrel_flag = (cfg->flags & MR_F_UNRELIABLE) ? 1u : 0u;
   D.safety = (cfg->flags & MR_F_SAFETY) ? 1u : 0u;
   D.bugs = cfg->flags & (MR_F_BUG_VOTE_TWICE | MR_F_BUG_VOTE_STALE | MR_F_BUG_NO_PREV_CHECK |
-                         MR_F_BUG_NO_DEDUP | MR_F_BUG_STALE_READ);
+                         MR_F_BUG_NO_DEDUP | MR_F_BUG_STALE_READ | MR_F_BUG_NO_APPLY_CHECK);
   D.links = kv_gen(cfg->scenario).part ? 1u : 0u;  // server-link cuts (CS_CUT) can exist
   D.lin15 = mr_scn_is_lin15(scn) ? 1u : 0u;  // generic_test_linearizability layout (SEMANTICS §9b)
   D.trace_clusters = (cfg->flags & MR_F_TRACE) ? cfg->trace_clusters : 0u;
@@ -363,8 +363,12 @@ static int mr_batch_create_impl(const mr_cfg* cfg, mr_batch** out) {
   }
   if (D.safety) add(&D.led, (size_t)LED_W * C);
   add(&D.trace, (size_t)D.trace_clusters * D.trace_cap);
+  add(&D.tdig, (size_t)D.trace_clusters * D.trace_cap);       // apply digests (ABI 4)
+  add(&D.tapp, (size_t)D.trace_clusters * D.trace_cap * 2u);  // KV applies (ABI 4)
+  add(&D.adig, (size_t)D.trace_clusters * MR_MAX_NODES * 2u);
   add(&D.remaining, 2);
   add(&D.prof, PROF_SLOTS);
+  add(&D.guard, 4);
   add(&D.tfr, (size_t)TF_Q * C);
   size_t total = 0;
   for (auto& it : items) total += (it.bytes + 255) & ~size_t(255);
@@ -407,7 +411,8 @@ static int mr_batch_create_impl(const mr_cfg* cfg, mr_batch** out) {
     b->D.dcap = cfg->tape_cap;
     b->D.tape_mode = 2;
   }
-  if (hipMemset(b->D.prof, 0, PROF_SLOTS * sizeof(unsigned long long)) != hipSuccess) {
+  if (hipMemset(b->D.prof, 0, PROF_SLOTS * sizeof(unsigned long long)) != hipSuccess ||
+      hipMemset(b->D.guard, 0, 4 * sizeof(uint32_t)) != hipSuccess) {
     mr_batch_destroy(b);
     return set_err("hipMemset failed");
   }
@@ -442,6 +447,11 @@ static int enqueue_reset(mr_batch* b, uint64_t seed_base) {
   HIPCHK(hipMemsetAsync(b->D.stor, 0, (size_t)b->D.C * b->D.apply_cap * sizeof(SE), b->stream));
   if (b->D.led)
     HIPCHK(hipMemsetAsync(b->D.led, 0, (size_t)b->D.C * LED_W * sizeof(uint32_t), b->stream));
+  if (b->D.trace_clusters) {  // apply digests: every node starts at 0 (valid), no record yet
+    HIPCHK(hipMemsetAsync(b->D.tdig, 0, (size_t)b->D.trace_clusters * b->D.trace_cap * 8u, b->stream));
+    HIPCHK(hipMemsetAsync(b->D.tapp, 0, (size_t)b->D.trace_clusters * b->D.trace_cap * 16u, b->stream));
+    HIPCHK(hipMemsetAsync(b->D.adig, 0, (size_t)b->D.trace_clusters * MR_MAX_NODES * 16u, b->stream));
+  }
   if (b->D.kv32)
     HIPCHK(hipMemsetAsync(b->D.kv32, 0, (size_t)b->D.C * b->D.n * KVREC * sizeof(uint32_t), b->stream));
   if (b->D.lin32)
@@ -538,6 +548,13 @@ int mr_batch_run(mr_batch* b, uint64_t max_events_per_call, mr_run_stats* st) {
     }
   }
   b->D.c0 = 0;
+#if MR_GUARD
+  uint32_t g[4];
+  HIPCHK(hipMemcpy(g, b->D.guard, sizeof g, hipMemcpyDeviceToHost));
+  if (g[0])
+    return set_err("MR_GUARD: index " + std::to_string(g[2]) + " out of range " + std::to_string(g[3]) +
+                   " (tag " + std::to_string(g[0]) + ", cluster " + std::to_string(g[1]) + ")");
+#endif
   s.wall_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   // events processed and clusters left: sums over the per-cluster counters (cheap reduce)
   mr_counters c;
@@ -647,6 +664,7 @@ int mr_batch_counters(mr_batch* b, mr_counters* out) {
   out->kv_lin_checked = h[CNT__N + 106];
   out->log_writes = h[CNT_LOG_WRITES];
   out->entries_materialized = h[CNT_MATERIALIZED];
+  out->coop_entries = h[CNT_COOP];
   out->first_fail_code = 0;
   if (out->first_fail_cluster != ~0ull) {
     uint32_t code = 0;
@@ -669,6 +687,39 @@ int mr_trace_get(mr_batch* b, uint32_t k, mr_event* out, size_t cap, size_t* n) 
                    hipMemcpyDeviceToHost));
   *n = m;
   return 0;
+}
+
+int mr_trace_digests(mr_batch* b, uint32_t k, uint64_t* out, size_t cap, size_t* n) {
+  if (!b || !out || !n) return set_err("null argument");
+  if (k >= b->D.trace_clusters) return set_err("cluster not traced");
+  HIPCHK(hipSetDevice(b->cfg.device));
+  HIPCHK(hipStreamSynchronize(b->stream));
+  uint32_t tn = 0;
+  HIPCHK(hipMemcpy(&tn, b->D.cs32 + CS_IDX(CS_TRACEN, k, b->D.C), 4, hipMemcpyDeviceToHost));
+  size_t m = tn < b->D.trace_cap ? tn : b->D.trace_cap;
+  if (m > cap) m = cap;
+  HIPCHK(hipMemcpy(out, b->D.tdig + (size_t)k * b->D.trace_cap, m * sizeof(uint64_t),
+                   hipMemcpyDeviceToHost));
+  *n = m;
+  return 0;
+}
+
+int mr_trace_applies(mr_batch* b, uint32_t k, uint64_t* out, size_t cap, size_t* n) {
+  if (!b || !out || !n) return set_err("null argument");
+  if (k >= b->D.trace_clusters) return set_err("cluster not traced");
+  HIPCHK(hipSetDevice(b->cfg.device));
+  HIPCHK(hipStreamSynchronize(b->stream));
+  size_t m = cap < b->D.trace_cap ? cap : b->D.trace_cap;
+  HIPCHK(hipMemcpy(out, b->D.tapp + (size_t)k * b->D.trace_cap * 2u, m * 2u * sizeof(uint64_t),
+                   hipMemcpyDeviceToHost));
+  while (m && !out[2 * (m - 1)]) m--;
+  *n = m;
+  return 0;
+}
+
+const char* mr_batch_kernel(const mr_batch* b) {
+  if (!b) return "";
+  return b->D.tape_mode ? "step_kernel_tape" : b->D.pool ? "pool_kernel" : "step_kernel";
 }
 
 uint32_t mr_decision_word(uint32_t v, uint32_t lo, uint32_t hi) {

@@ -70,18 +70,41 @@ struct X {
   uint32_t ls;  // pool_kernel: the cluster's pool slot (its LDS column)
 };
 
+// MR_GUARD (a debug build, build.build_guard; tests/test_guard.py): every computed index into a
+// per-cluster global array is checked against its bound. A violation is recorded in D.guard
+// {tag, cluster, index, bound} with plain vector stores and the index replaced by 0, so the run
+// ends with an error from mr_batch_run instead of a memory fault. Product builds: GI(i) = i.
+#ifndef MR_GUARD
+#define MR_GUARD 0
+#endif
+enum : uint32_t { G_NODE = 1, G_MSG, G_LOG, G_KT_SLOT, G_KT_FIELD, G_KWK, G_KV, G_CFG_S, G_CFG_J,
+                  G_OP, G_STOR, G_CHURN, G_LINJ, G_LKEY, G_PAY };
+#if MR_GUARD
+__device__ __noinline__ uint32_t guard_bad(uint32_t* g, uint32_t tag, uint32_t c, uint32_t i,
+                                           uint32_t n) {
+  g[1] = c; g[2] = i; g[3] = n;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+  g[0] = tag;
+  return 0u;
+}
+#define GI(i, n, tag) \
+  ((uint32_t)(i) < (uint32_t)(n) ? (uint32_t)(i) : guard_bad(D.guard, (tag), x.c, (uint32_t)(i), (uint32_t)(n)))
+#else
+#define GI(i, n, tag) (i)
+#endif
+
 // field accessors (32-bit element offsets, checked at batch creation)
 #define CS(f) D.cs32[CS_IDX(f, x.c, D.C)]
 #define C64(f) D.cs64[C64_IDX(f, x.c, D.C)]
-#define NDP(d) (D.nd32 + ((size_t)x.c * D.n + (d)) * NREC)  // node d's 128-B record
+#define NDP(d) (D.nd32 + ((size_t)x.c * D.n + GI(d, D.n, G_NODE)) * NREC)  // node d's 128-B record
 #define ND(f, d) NDP(d)[f]
 #define NSV(d) (*reinterpret_cast<uint64_t*>(NDP(d) + NF_SNAPV))
 #define PR(f, d, p) NDP(d)[NR_PEER + (f) * MR_MAX_NODES + (p)]
-#define MSP(s) (D.ms32 + ((size_t)x.c * D.M + (s)) * MREC)  // message slot s's 32-B record
+#define MSP(s) (D.ms32 + ((size_t)x.c * D.M + GI(s, D.M, G_MSG)) * MREC)  // message slot s's 32-B record
 #define MS32(f, s) MSP(s)[f]
 #define MSV(s) (*reinterpret_cast<uint64_t*>(MSP(s) + MF_V))
-#define MKEY(s) D.mkey[(size_t)(s) * D.C + x.c]
-#define TMR(d) D.tmr[(size_t)(d) * D.C + x.c]
+#define MKEY(s) D.mkey[(size_t)GI(s, D.M, G_MSG) * D.C + x.c]
+#define TMR(d) D.tmr[(size_t)GI(d, D.n, G_NODE) * D.C + x.c]
 // message keys of the lane's cluster live in LDS during a launch: [slot][lane],
 // so a wave's 64 lanes read 64 consecutive u64 (conflict-free). Free slots hold
 // ~0, so the earliest-message scan is a branch-free min over all M slots.
@@ -122,9 +145,9 @@ extern __shared__ uint64_t s_keys_raw[];
 // key rows: one column per lane (step_kernel) or per pool slot (pool_kernel, x.ls)
 constexpr uint32_t KSTR = MR_POOL ? POOL_SLOTS : STEP_BLOCK;
 #if MR_POOL
-#define LK(s) s_keys[(s) * KSTR + x.ls]
+#define LK(s) s_keys[GI(s, D.M, G_LKEY) * KSTR + x.ls]
 #else
-#define LK(s) s_keys[(s) * KSTR + threadIdx.x]
+#define LK(s) s_keys[GI(s, D.M, G_LKEY) * KSTR + threadIdx.x]
 #endif
 // per-wave staging after the M key rows: 16 rows of 64 lanes (u32) for each wave of the block —
 // the send loop's next[p] / term at next[p] - 1, the appliers' and the AppendEntries receive's
@@ -252,7 +275,7 @@ DI void philox(const Dev& D, X& x, uint32_t c0, uint32_t c1, uint32_t c2, uint32
   w1 = w.y;
 }
 DI size_t logi(const Dev& D, const X& x, uint32_t d, uint32_t i) {
-  return ((size_t)x.c * D.n + d) * D.log_cap + (i & (D.log_cap - 1u));
+  return ((size_t)x.c * D.n + GI(d, D.n, G_LOG)) * D.log_cap + (i & (D.log_cap - 1u));
 }
 
 // One node's scalar state, loaded into registers at the start of an event
@@ -367,8 +390,38 @@ DI void rec8(const Dev& D, X& x, uint32_t w0, uint32_t w1, uint32_t w2, uint32_t
 DI void rec_node(const Dev& D, X& x, uint32_t cls, uint32_t kind, uint32_t d, uint32_t aux,
                  const NC& n) {
   uint32_t role = bit(x.alive, d) ? f_role(n.f) : R_DOWN;
+  const uint32_t idx = x.trace_n;
   rec8(D, x, x.now, cls | (kind << 8) | (d << 16) | (role << 24), aux, n.term, n.commit,
        n.applied, n.last, n.snap);
+  if (x.c < D.trace_clusters && idx < D.trace_cap) {  // the node's apply digest beside the record
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "agent");  // after this event's (helpers') adds
+    uint64_t* p = D.adig + ((size_t)x.c * MR_MAX_NODES + d) * 2u;
+    const uint64_t s = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint64_t inv = __hip_atomic_load(p + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    D.tdig[(size_t)x.c * D.trace_cap + idx] = inv ? ~0ull : s;
+  }
+}
+
+// ---- apply digests of traced clusters (ABI 4: mr_trace_digests, docs/SEMANTICS.md §7): per
+// node the sum of mr_apply_mix(i, value) over the entries it applied one by one, an invalid flag
+// once it installed a snapshot or restarted above index 0; trace builds only (c < trace_clusters)
+DI uint64_t amix(uint32_t i, uint64_t v) {  // include/madraft_sim.h mr_apply_mix
+  uint64_t z = v ^ ((uint64_t)i * 0x9E3779B97F4A7C15ull);
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+DI void adig_add(const Dev& D, uint32_t c, uint32_t node, uint32_t i, uint64_t v) {
+  if (c < D.trace_clusters)  // (a helper lane of the cooperative applier adds for its owner)
+    __hip_atomic_fetch_add(D.adig + ((size_t)c * MR_MAX_NODES + node) * 2u, amix(i, v),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+DI void adig_set(const Dev& D, uint32_t c, uint32_t node, bool invalid) {  // restart / install
+  if (c < D.trace_clusters) {
+    uint64_t* p = D.adig + ((size_t)c * MR_MAX_NODES + node) * 2u;
+    __hip_atomic_exchange(p, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_exchange(p + 1, invalid ? 1ull : 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
 }
 
 DI void rec_simple(const Dev& D, X& x, uint32_t cls, uint32_t kind) {
@@ -618,7 +671,7 @@ DI void materialize(const Dev& D, X& x, uint32_t L, uint32_t& pexp) {
     const uint32_t hdr = MS32(MF_HDR, s), k = hdr_k(hdr);
     if (hdr_type(hdr) != M_AE_REQ || hdr_src(hdr) != L || (hdr & HDR_MAT) || k == 0) continue;
     const uint32_t prev = MS32(MF_A, s);
-    LE* pp = D.pay + ((size_t)x.c * D.M + s) * D.K;
+    LE* pp = D.pay + ((size_t)x.c * D.M + GI(s, D.M, G_PAY)) * D.K;
     for (uint32_t j = 0; j < k; j++) pp[j] = D.log[logi(D, x, L, prev + 1 + j)];
     MS32(MF_HDR, s) = hdr | HDR_MAT;
     CADD(CNT_MATERIALIZED, k);
@@ -653,7 +706,7 @@ DI void storage_snapshot(const Dev& D, X& x, uint32_t i, uint32_t& slen, uint32_
   if (idx >= D.apply_cap) { fail(D, x, MR_FAIL_SIM_CAPACITY); return; }
   uint32_t nl = idx + 1;
   for (uint32_t j = nl; j < slen; j++) {
-    SE* e = D.stor + (size_t)x.c * D.apply_cap + j;
+    SE* e = D.stor + (size_t)x.c * D.apply_cap + GI(j, D.apply_cap, G_STOR);
     e->mask &= ~(1u << i);
   }
   slen = nl;
@@ -661,7 +714,7 @@ DI void storage_snapshot(const Dev& D, X& x, uint32_t i, uint32_t& slen, uint32_
 
 DI uint32_t n_committed(const Dev& D, X& x, uint32_t idx, uint64_t& v) {  // tester.rs:405-422
   if (idx >= D.apply_cap) { v = 0; return 0; }
-  const SE e = D.stor[(size_t)x.c * D.apply_cap + idx];
+  const SE e = D.stor[(size_t)x.c * D.apply_cap + GI(idx, D.apply_cap, G_STOR)];
   v = e.val;
   return (uint32_t)__builtin_popcount(e.mask);
 }
@@ -761,8 +814,12 @@ DI void node_apply(const Dev& D, X& x, uint32_t me, NC& d, uint32_t& kvready) {
       d.applied = i;
       if (i >= D.apply_cap) { fail(D, x, MR_FAIL_SIM_CAPACITY); return; }
       CADD(CNT_APPLIES, 1u);
-      if (cm[j] && csv[j] != ce[j].val) { fail(D, x, MR_FAIL_APPLY_MISMATCH); return; }  // tester.rs:384
+      if (cm[j] && csv[j] != ce[j].val && !(D.bugs & MR_F_BUG_NO_APPLY_CHECK)) {  // tester.rs:384
+        fail(D, x, MR_FAIL_APPLY_MISMATCH);
+        return;
+      }
       if (i > len) { fail(D, x, MR_FAIL_APPLY_OUT_OF_ORDER); return; }  // tester.rs:393
+      adig_add(D, x.c, me, i, ce[j].val);
       if (i == len) {
         sb[i] = SE{ce[j].val, cm[j] | (1u << me), ce[j].term};
         len++;
@@ -869,7 +926,7 @@ DI void node_apply_coop(const Dev& D, X& x, uint32_t me, NC& d) {
     const bool inb = mine && i < D.apply_cap;
     if (inb) {
       e = D.log[((size_t)oc * D.n + ome) * D.log_cap + (i & (D.log_cap - 1u))];
-      s = D.stor[(size_t)oc * D.apply_cap + i];
+      s = D.stor[(size_t)oc * D.apply_cap + GI(i, D.apply_cap, G_STOR)];
     }
     // the entry is consumed here on every path (not only where it is stored): a load left pending
     // past the applier makes the step loop's next write to that register wait on vmcnt(0)
@@ -877,7 +934,8 @@ DI void node_apply_coop(const Dev& D, X& x, uint32_t me, NC& d) {
     uint32_t key = ~0u;
     if (mine) {
       if (!inb) key = (i << 2) | 0u;                                    // SIM_CAPACITY
-      else if (s.mask && s.val != e.val) key = (i << 2) | 1u;           // APPLY_MISMATCH
+      else if (s.mask && s.val != e.val && !(D.bugs & MR_F_BUG_NO_APPLY_CHECK))
+        key = (i << 2) | 1u;                                            // APPLY_MISMATCH
       else if (i == obase && obase > olen) key = (i << 2) | 2u;         // APPLY_OUT_OF_ORDER
     }
     // the LDS exchange only once some entry of the wave has failed (wave-uniform flag)
@@ -892,8 +950,9 @@ DI void node_apply_coop(const Dev& D, X& x, uint32_t me, NC& d) {
     if (mine) {
       const uint32_t fk = anyfail ? fkw[o] : ~0u;
       const uint32_t f = fk == ~0u ? ~0u : fk >> 2;
+      if (i < f) adig_add(D, oc, ome, i, e.val);
       if (i < f && i >= olen)  // i == len in node_apply's walk: appended
-        D.stor[(size_t)oc * D.apply_cap + i] = SE{e.val, s.mask | (1u << ome), e.term};
+        D.stor[(size_t)oc * D.apply_cap + GI(i, D.apply_cap, G_STOR)] = SE{e.val, s.mask | (1u << ome), e.term};
       if (snapmode && i < f && (i + 1u) % 10u == 0u) {
         // the last snapshot index of the applied range [obase, min(oend, f - 1)]
         const uint32_t hi = f <= oend ? f - 1u : oend;
@@ -966,7 +1025,7 @@ DI void safety_on_leader(const Dev& D, X& x, uint32_t me, const NC& d) {
   const uint32_t j = CNT_GET(CNT_MAX_INDEX);
   const uint32_t w = *lw;
   const LE le = D.log[logi(D, x, me, j)];
-  const SE se = D.stor[(size_t)x.c * D.apply_cap + j];
+  const SE se = D.stor[(size_t)x.c * D.apply_cap + GI(j, D.apply_cap, G_STOR)];
   if ((w >> (t & 31u)) & 1u) { fail(D, x, MR_FAIL_SAFETY_ELECTION); return; }
   *lw = w | (1u << (t & 31u));
   if (j > d.snap && (j > d.last || le.val != se.val || le.term != se.term))
@@ -1076,6 +1135,7 @@ DI bool ae_recv_coop(const Dev& D, X& x, uint32_t me, NC& d, uint32_t src, bool 
                                                // pass 2: rows 4 / 5 = rs / term of the last written
   const uint32_t lane = lane64();
   const uint32_t cnt = k > jr ? k - jr : 0u;
+  if (cnt) CADD(CNT_COOP, cnt);  // entries handed to the wave (mr_counters.coop_entries)
   // entries from jp on are past our log (index ma + 1 + j > last): never a match
   const uint32_t jp = d.last - ma;  // prev <= last and ma <= prev (a snapshot skip raises prev)
   const uint32_t f0 = wrote ? jr : (jp > jr ? (jp < k ? jp : k) : jr);
@@ -1114,7 +1174,7 @@ DI bool ae_recv_coop(const Dev& D, X& x, uint32_t me, NC& d, uint32_t src, bool 
         // the owner's jr (a helper's own first-batch end differs when its payload is shorter)
         const uint32_t ojr = opk >> 20, j = ojr + jx, i = oma + 1u + j, ri = i & (D.log_cap - 1u);
         const uint32_t ome = (opk >> 14) & 7u, osrc = (opk >> 9) & 31u, oslot = (opk >> 1) & 255u;
-        const LE pe = (opk & 1u) ? D.pay[((size_t)oc * D.M + oslot) * D.K + j]
+        const LE pe = (opk & 1u) ? D.pay[((size_t)oc * D.M + GI(oslot, D.M, G_PAY)) * D.K + GI(j, D.K, G_PAY)]
                                  : D.log[((size_t)oc * D.n + osrc) * D.log_cap + ri];
         const LE ow = D.log[((size_t)oc * D.n + ome) * D.log_cap + ri];
         const uint32_t ot = i == olast ? olastt : ow.term, ors = i == olast ? olrs : ow.rs;
@@ -1174,7 +1234,7 @@ DI bool ae_recv_coop(const Dev& D, X& x, uint32_t me, NC& d, uint32_t src, bool 
       if (o < 64u) {
         const uint32_t of = ofe & 255u, j = of + jx, i = oma + 1u + j, ri = i & (D.log_cap - 1u);
         const uint32_t ome = (opk >> 14) & 7u, osrc = (opk >> 9) & 31u, oslot = (opk >> 1) & 255u;
-        const LE pe = (opk & 1u) ? D.pay[((size_t)oc * D.M + oslot) * D.K + j]
+        const LE pe = (opk & 1u) ? D.pay[((size_t)oc * D.M + GI(oslot, D.M, G_PAY)) * D.K + GI(j, D.K, G_PAY)]
                                  : D.log[((size_t)oc * D.n + osrc) * D.log_cap + ri];
         const uint32_t rs = pe.rs >= oma + 1u + of ? pe.rs : orsf;
         D.log[((size_t)oc * D.n + ome) * D.log_cap + ri] = LE{pe.term, rs, pe.val};
@@ -1346,7 +1406,7 @@ DI void node_event(const Dev& Darg, X& x, bool is_msg, uint32_t tnode, uint32_t 
           prev = d.snap; pterm = d.snapt;
         }
         if (prev > d.last) { rb = d.last + 1; break; }
-        const LE* pp = D.pay + ((size_t)x.c * D.M + slot) * D.K;
+        const LE* pp = D.pay + ((size_t)x.c * D.M + GI(slot, D.M, G_PAY)) * D.K;
         const bool mat = (hdr_bits & HDR_MAT) != 0u;
         // one batch of independent loads: prev's term, then AC payload entries
         // (sender's ring or materialized copy) and our terms at their indices
@@ -1444,6 +1504,7 @@ DI void node_event(const Dev& Darg, X& x, bool is_msg, uint32_t tnode, uint32_t 
           }
           d.snap = idx; d.snapt = mb; NSV(me) = MSV(slot);
           d.commit = idx; d.applied = idx;
+          adig_set(D, x.c, me, true);
           storage_snapshot(D, x, me, d.slen, idx);
           if (x.code != RUN) return;
           if constexpr (kv_gen(S).maxraft > 0) {
@@ -1624,6 +1685,7 @@ DI void t_start1(const Dev& D, X& x, uint32_t i) {  // tester.rs:293-327, raft.r
   n.f = f_set(f_set(n.f, 0, 2, R_F), 16, 8, 0u);
   n.commit = n.snap;
   n.applied = n.snap;
+  adig_set(D, x.c, i, n.snap != 0u);
   if (!D.null_raft) reset_timer(D, x, i, n);
   store_node(D, x, i, n);
 }

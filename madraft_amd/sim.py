@@ -48,6 +48,12 @@ def lib():
     L.mr_batch_counters.argtypes = [C.c_void_p, C.POINTER(MrCounters)]
     L.mr_trace_get.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_size_t,
                                C.POINTER(C.c_size_t)]
+    L.mr_trace_digests.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_size_t,
+                                   C.POINTER(C.c_size_t)]
+    L.mr_trace_applies.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_size_t,
+                                   C.POINTER(C.c_size_t)]
+    L.mr_batch_kernel.argtypes = [C.c_void_p]
+    L.mr_batch_kernel.restype = C.c_char_p
     L.mr_batch_set_decisions.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t]
     L.mr_batch_get_decisions.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_size_t,
                                          C.POINTER(C.c_size_t)]
@@ -206,6 +212,27 @@ class Batch:
         n = C.c_size_t()
         _check(lib().mr_trace_get(self._b, int(k), out.ctypes.data, cap, C.byref(n)))
         return out[: n.value]
+
+    def trace_digests(self, k, cap=None):
+        """mr_trace_digests: per record of trace(k), its node's apply digest (ABI 4)."""
+        cap = cap or int(self.cfg.trace_cap)
+        out = np.empty(cap, np.uint64)
+        n = C.c_size_t()
+        _check(lib().mr_trace_digests(self._b, int(k), out.ctypes.data, cap, C.byref(n)))
+        return out[: n.value]
+
+    def trace_applies(self, k, cap=None):
+        """mr_trace_applies: [n, 2] (command, key hash after it) per log index (ABI 4)."""
+        cap = cap or int(self.cfg.trace_cap)
+        out = np.zeros((cap, 2), np.uint64)
+        n = C.c_size_t()
+        _check(lib().mr_trace_applies(self._b, int(k), out.ctypes.data, cap, C.byref(n)))
+        return out[: n.value]
+
+    @property
+    def kernel(self):
+        """mr_batch_kernel: "pool_kernel", "step_kernel" or "step_kernel_tape"."""
+        return lib().mr_batch_kernel(self._b).decode()
 
 
 def replay(test, decisions, trace_cap=1 << 16, cluster_base=0, **kw):

@@ -163,6 +163,9 @@ typedef struct {
   uint32_t l15_j[LIN_CLI]; /* client cli's next token j, carried over iterations (tokens unique) */
   uint8_t link[MR_MAX_NODES]; /* server links (connect2/disconnect2): bit j of link[i] = i~j */
   uint64_t tape_row; int tape_on; uint64_t tape_pos; /* keyed decisions: row, count (§12) */
+  /* apply digests (ABI 4 mr_trace_digests): per node the sum of mr_apply_mix over the entries it
+   * applied one by one, invalid once it installed a snapshot or restarted above index 0 */
+  uint64_t adig[MR_MAX_NODES]; uint8_t ainv[MR_MAX_NODES];
   uint8_t ccut[CK_SLOTS];     /* clerk links cut: bit j of ccut[k] = clerk host 8 + k !~ server j */
   OCfg* cfgs; /* [MR_MAX_NODES][CFG_CAP] */
   OOp* ops;   /* [OP_CAP] */
@@ -170,6 +173,8 @@ typedef struct {
   /* results */
   mro_result r;
   mr_event* trace; size_t trace_cap, n_trace;
+  uint64_t* tdig; /* [trace_cap] the apply digest beside each record (0: not a node event) */
+  uint64_t* tapp; /* [trace_cap][2] KV command, key hash after its first application */
   jmp_buf jb;
 } OSim;
 
@@ -182,6 +187,7 @@ static void rec_push(OSim* s, const mr_event* e) {
   for (int i = 0; i < 8; i++) { h ^= w[i]; h *= 0x100000001B3ull; }
   s->r.digest = h;
   if (s->trace && s->n_trace < s->trace_cap) s->trace[s->n_trace] = *e;
+  if (s->tdig && s->n_trace < s->trace_cap) s->tdig[s->n_trace] = 0;
   s->n_trace++;
 }
 
@@ -192,7 +198,9 @@ static void rec_node(OSim* s, uint32_t cls, uint32_t kind, uint32_t node, uint32
   e.role = (uint8_t)(d->alive ? d->role : R_DOWN);
   e.aux = aux; e.term = d->term; e.commit = d->commit; e.applied = d->applied;
   e.last = d->last; e.snap = d->snap_idx;
+  const size_t idx = s->n_trace;
   rec_push(s, &e);
+  if (s->tdig && idx < s->trace_cap) s->tdig[idx] = s->ainv[node] ? ~0ull : s->adig[node];
 }
 
 static void rec_simple(OSim* s, uint32_t cls, uint32_t kind) {
@@ -343,7 +351,8 @@ static void net_send(OSim* s, uint32_t src, uint32_t dst, OMsg* m) {
 static void push_and_check(OSim* s, uint32_t i, uint32_t idx, uint64_t v, uint32_t term) {
   if (idx >= s->cfg.apply_cap) t_fail(s, MR_FAIL_SIM_CAPACITY);
   s->r.applies++;
-  if (s->mask[idx] && s->sval[idx] != v) t_fail(s, MR_FAIL_APPLY_MISMATCH); /* :384 */
+  if (s->mask[idx] && s->sval[idx] != v && !(s->cfg.flags & MR_F_BUG_NO_APPLY_CHECK))
+    t_fail(s, MR_FAIL_APPLY_MISMATCH); /* :384 */
   if (idx > s->slen[i]) t_fail(s, MR_FAIL_APPLY_OUT_OF_ORDER);              /* :393 */
   if (idx == s->slen[i]) {
     s->sval[idx] = v;
@@ -537,6 +546,9 @@ static void kv_apply(OSim* s, uint32_t me, uint32_t i, uint64_t v) {
     }
     s->kv_dedup[me][clerk] = seq;
   }
+  if (!s->ctrl_mode && s->tapp && i < s->trace_cap && !s->tapp[2 * i]) { /* mr_trace_applies */
+    s->tapp[2 * i] = v; s->tapp[2 * i + 1] = k->h;
+  }
   for (uint32_t p = 0; p < KV_PEND; p++) { /* answered at the end of the event (kv_flush) */
     OPend* q = &s->pend[me][p];
     if (!q->used || q->ready || q->idx != i) continue;
@@ -627,6 +639,7 @@ static void node_apply(OSim* s, uint32_t me) {
     uint32_t i = ++d->applied;
     uint64_t v = d->lval[lpos(s, i)];
     push_and_check(s, me, i, v, d->lterm[lpos(s, i)]);
+    s->adig[me] += mr_apply_mix(i, v);
     if (s->kv_mode) kv_apply(s, me, i, v);
     if (s->kv_maxraft && i % KV_SNAP_EVERY == 0 && i > d->snap_idx &&
         raft_state_size(d) >= s->kv_maxraft / 2) kv_snapshot(s, me, i);
@@ -872,6 +885,7 @@ static void deliver(OSim* s, OMsg* m) {
         if (!(idx <= d->last && term_at(s, d, idx) == m->b)) d->last = idx;
         d->snap_idx = idx; d->snap_term = m->b; d->snap_val = m->v;
         d->commit = idx; d->applied = idx;
+        s->ainv[me] = 1;
         storage_snapshot(s, me, idx);
         if (s->kv_maxraft) kv_install(s, me, idx);
         s->r.installs++;
@@ -1022,6 +1036,7 @@ static void t_start1(OSim* s, uint32_t i) { /* tester.rs:293-327 + raft.rs:108-1
   ONode* d = &s->nd[i];
   d->alive = 1; d->inc++; d->role = R_F; d->votes = 0;
   d->commit = d->snap_idx; d->applied = d->snap_idx;
+  s->adig[i] = 0; s->ainv[i] = d->snap_idx != 0;
   if (!s->null_raft) reset_timer(s, i);
 }
 
@@ -2589,6 +2604,7 @@ static void sim_reset(OSim* s, uint64_t cluster) {
   memset(&s->r, 0, sizeof s->r);
   s->r.digest = 0xCBF29CE484222325ull;
   s->n_trace = 0;
+  memset(s->adig, 0, sizeof s->adig); memset(s->ainv, 0, sizeof s->ainv);
   uint64_t row = cluster - s->cfg.cluster_base;
   s->tape_row = row;
   s->tape_on = g_tape_mode == 2 || (g_tape_mode == 1 && row < g_dec_rows);
@@ -2640,9 +2656,20 @@ int mro_set_decisions(int mode, const mr_decision* d, uint64_t n, uint64_t rows,
 
 int mro_run_cluster(const mr_cfg* cfg, uint64_t cluster, mro_result* out, mr_event* trace,
                     size_t trace_cap, size_t* n_trace) {
+  return mro_run_cluster_dig(cfg, cluster, out, trace, NULL, trace_cap, n_trace);
+}
+
+int mro_run_cluster_dig(const mr_cfg* cfg, uint64_t cluster, mro_result* out, mr_event* trace,
+                        uint64_t* tdig, size_t trace_cap, size_t* n_trace) {
+  return mro_run_cluster_kv(cfg, cluster, out, trace, tdig, NULL, trace_cap, n_trace);
+}
+
+int mro_run_cluster_kv(const mr_cfg* cfg, uint64_t cluster, mro_result* out, mr_event* trace,
+                       uint64_t* tdig, uint64_t* tapp, size_t trace_cap, size_t* n_trace) {
   OSim* s = (OSim*)malloc(sizeof(OSim));
   if (!s || sim_alloc(s, cfg) != 0) { free(s); return -1; }
-  s->trace = trace; s->trace_cap = trace_cap;
+  s->trace = trace; s->trace_cap = trace_cap; s->tdig = tdig; s->tapp = tapp;
+  if (tapp) memset(tapp, 0, trace_cap * 2 * sizeof(uint64_t));
   sim_run(s, cfg->cluster_base + cluster);
   if (out) *out = s->r;
   if (n_trace) *n_trace = s->n_trace;

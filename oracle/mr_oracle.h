@@ -44,6 +44,14 @@ typedef struct mro_result {
  * trace_cap records, *n_trace the number written. Returns 0 or <0 on a bad cfg. */
 int mro_run_cluster(const mr_cfg* cfg, uint64_t cluster, mro_result* out,
                     mr_event* trace, size_t trace_cap, size_t* n_trace);
+/* The same, with tdig[trace_cap] (optional) receiving each record's apply digest (ABI 4
+ * mr_trace_digests). */
+int mro_run_cluster_dig(const mr_cfg* cfg, uint64_t cluster, mro_result* out, mr_event* trace,
+                        uint64_t* tdig, size_t trace_cap, size_t* n_trace);
+/* ... and tapp[trace_cap][2] (optional) receiving the KV commands as applied (ABI 4
+ * mr_trace_applies). */
+int mro_run_cluster_kv(const mr_cfg* cfg, uint64_t cluster, mro_result* out, mr_event* trace,
+                       uint64_t* tdig, uint64_t* tapp, size_t trace_cap, size_t* n_trace);
 
 /* Run clusters [first, first+count) and fill per-cluster arrays (any may be NULL). */
 int mro_run_batch(const mr_cfg* cfg, uint64_t first, uint64_t count,

@@ -34,6 +34,12 @@ class Oracle:
         L = C.CDLL(path)
         L.mro_run_cluster.argtypes = [C.POINTER(MrCfg), C.c_uint64, C.POINTER(MroResult),
                                       C.c_void_p, C.c_size_t, C.POINTER(C.c_size_t)]
+        L.mro_run_cluster_dig.argtypes = [C.POINTER(MrCfg), C.c_uint64, C.POINTER(MroResult),
+                                          C.c_void_p, C.c_void_p, C.c_size_t,
+                                          C.POINTER(C.c_size_t)]
+        L.mro_run_cluster_kv.argtypes = [C.POINTER(MrCfg), C.c_uint64, C.POINTER(MroResult),
+                                         C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t,
+                                         C.POINTER(C.c_size_t)]
         L.mro_run_batch.argtypes = [C.POINTER(MrCfg), C.c_uint64, C.c_uint64, C.c_void_p,
                                     C.c_void_p, C.c_void_p, C.POINTER(MroResult)]
         L.mro_philox4x32_10.argtypes = [C.POINTER(C.c_uint32 * 4), C.POINTER(C.c_uint32 * 2),
@@ -74,6 +80,33 @@ class Oracle:
                                     C.byref(n))
         assert rc == 0, "bad config"
         return r.to_dict(), tr[: min(n.value, trace_cap)] if trace_cap else None
+
+    def run_cluster_dig(self, cfg, cluster, trace_cap):
+        """run_cluster with each trace record's apply digest (ABI 4 mr_trace_digests)."""
+        r = MroResult()
+        n = C.c_size_t()
+        tr = np.empty(max(trace_cap, 1), EVENT_DTYPE)
+        dg = np.empty(max(trace_cap, 1), np.uint64)
+        rc = self.L.mro_run_cluster_dig(C.byref(cfg), int(cluster), C.byref(r), tr.ctypes.data,
+                                        dg.ctypes.data, int(trace_cap), C.byref(n))
+        assert rc == 0, "bad config"
+        m = min(n.value, trace_cap)
+        return r.to_dict(), tr[:m], dg[:m]
+
+    def run_cluster_kv(self, cfg, cluster, trace_cap):
+        """run_cluster with the KV commands as applied (ABI 4 mr_trace_applies): (result,
+        trace, applies[n, 2])."""
+        r = MroResult()
+        n = C.c_size_t()
+        tr = np.empty(max(trace_cap, 1), EVENT_DTYPE)
+        ap = np.zeros((max(trace_cap, 1), 2), np.uint64)
+        rc = self.L.mro_run_cluster_kv(C.byref(cfg), int(cluster), C.byref(r), tr.ctypes.data,
+                                       None, ap.ctypes.data, int(trace_cap), C.byref(n))
+        assert rc == 0, "bad config"
+        m = len(ap)
+        while m and not ap[m - 1, 0]:
+            m -= 1
+        return r.to_dict(), tr[: min(n.value, trace_cap)], ap[:m]
 
     def recording(self, rows, cap):
         """Context: the following runs record every draw as a keyed decision (SEMANTICS §12);

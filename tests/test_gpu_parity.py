@@ -39,13 +39,17 @@ def compare(hip, oracle, test, clusters, traced=4, first=0, oracle_codes=False, 
         code, t, dig = b.verdicts()
         cnt = b.counters()
         traces = [b.trace(k) for k in range(traced)]
+        tdigs = [b.trace_digests(k) for k in range(traced)]
         cfg = b.cfg
     ocode, ot, odig, osum = oracle.run_batch(cfg, 0, clusters)
     for k in range(traced):
-        _, otr = oracle.run_cluster(cfg, k, trace_cap=int(cfg.trace_cap))
+        _, otr, odg = oracle.run_cluster_dig(cfg, k, int(cfg.trace_cap))
         if not np.array_equal(traces[k], otr):
             i, g, o = first_diff(traces[k], otr)
             pytest.fail(f"{test} cluster {k}: trace differs at record {i}: gpu={g} oracle={o}")
+        if not np.array_equal(tdigs[k], odg):
+            i = int(np.nonzero(tdigs[k] != odg)[0][0])
+            pytest.fail(f"{test} cluster {k}: apply digest differs at record {i}: {traces[k][i]}")
     bad = np.nonzero((code != ocode) | (t != ot) | (dig != odig))[0]
     assert bad.size == 0, (f"{test}: {bad.size} clusters differ, first {bad[0]}: "
                            f"gpu=({code[bad[0]]},{t[bad[0]]}) oracle=({ocode[bad[0]]},{ot[bad[0]]})")
@@ -158,16 +162,24 @@ def test_small_capacities_fail_identically(hip, oracle):
     compare(hip, oracle, "figure_8_unreliable_2c", 128, log_cap=64, msg_slots=6, ae_max=2)
 
 
-@pytest.mark.parametrize("kw", [dict(log_cap=32, msg_slots=12), dict(log_cap=64, flags=_abi.MR_F_SAFETY),
-                                dict(flags=_abi.MR_F_SAFETY | _abi.MR_F_BUG_NO_PREV_CHECK)])
-def test_cooperative_append_receive(hip, oracle, kw):
-    """The cooperative AppendEntries receive (MR_AE_COOP: a payload's entries after the first
-    batch spread over the wave): full 16-entry payloads hitting a tiny log ring (SIM_CAPACITY
-    part-way through the spread entries, write-guard materializations), MR_F_SAFETY log
-    matching, and a Raft without the prev check (whose logs diverge) — all equal to the
-    oracle's sequential walk."""
-    code, cnt = compare(hip, oracle, "figure_8_unreliable_2c", 512, traced=3, **kw)
-    assert cnt["log_writes"] > 0
+@pytest.mark.parametrize("test,kw", [
+    ("figure_8_unreliable_2c", dict(nodes=7, log_cap=32, msg_slots=12)),
+    ("figure_8_unreliable_2c", dict(nodes=7, log_cap=64, flags=_abi.MR_F_SAFETY)),
+    ("figure_8_unreliable_2c", dict(nodes=8, flags=_abi.MR_F_SAFETY | _abi.MR_F_BUG_NO_PREV_CHECK)),
+    ("snapshot_install_unreliable_2d", dict(nodes=7)),
+    ("figure_8_unreliable_2c", dict(pool=False, log_cap=32, msg_slots=12))])
+def test_cooperative_append_receive(hip, oracle, monkeypatch, test, kw):
+    """The cooperative AppendEntries receive of the per-lane step kernel (a payload's entries
+    after the first batch spread over the wave; the pool kernel receives sequentially, so these
+    cases run where the step kernel does: 7- and 8-node clusters, or MR_POOL=0): full 16-entry
+    payloads hitting a tiny log ring (SIM_CAPACITY part-way through the spread entries,
+    write-guard materializations), MR_F_SAFETY log matching, a Raft without the prev check
+    (whose logs diverge) and snapshot compaction under the spread — all equal to the oracle's
+    sequential walk, and the spread path taken (coop_entries, ABI 4)."""
+    if not kw.pop("pool", True):
+        monkeypatch.setenv("MR_POOL", "0")
+    code, cnt = compare(hip, oracle, test, 512, traced=3, **kw)
+    assert cnt["log_writes"] > 0 and cnt["coop_entries"] > 0
 
 
 def test_step_budget_independence(hip):

@@ -11,7 +11,11 @@ node's role / term / commit / applied / last / snapshot index), and hold for any
   never decreases either way;
 * leader append-only: while a node leads in a term, its last index never decreases;
 * leader completeness: a new leader's log reaches every index committed before its election;
-* commit quorum: every committed index is within the logs of a majority (check_commit_quorum).
+* commit quorum: every committed index is within the logs of a majority (check_commit_quorum);
+* state-machine safety by value (check_apply_digests): nodes that report the same applied index
+  report the same apply digest — the sum of mr_apply_mix(i, command_i) over the entries they
+  applied (ABI 4 mr_trace_digests), so two nodes that applied different commands at any index
+  up to it disagree.
 
 CPU: oracle traces of many seeds over the BASELINE shapes; GPU: the HIP path's own traces.
 """
@@ -57,6 +61,24 @@ def check_commit_quorum(tr, n):
             f"t={t}: index {cmax} committed but on fewer than {maj} logs: {last.tolist()}"
 
 
+def check_apply_digests(tr, dg):
+    """State-machine safety by value (Raft paper Figure 3): every node that has applied up to
+    index a has applied the same commands 1..a, so node records with equal `applied` carry equal
+    apply digests (a node that installed a snapshot or restarted above 0 reports none). Returns
+    the number of (applied index) groups with two or more records compared."""
+    node = (tr["cls"] <= 1) & (tr["node"] < 8) & (dg != _abi.DIGEST_INVALID)
+    seen, compared = {}, set()
+    for ev, d in zip(tr[node], dg[node]):
+        a = int(ev["applied"])
+        if a in seen:
+            assert seen[a] == int(d), f"t={int(ev['time_us'])}: node {int(ev['node'])} applied 1..{a} with other commands"
+            compared.add(a)
+        else:
+            seen[a] = int(d)
+    assert seen.get(0, 0) == 0, "an empty applied prefix has digest 0"
+    return len(compared)
+
+
 def check_trace(tr, test, n=None):
     assert (np.diff(tr["time_us"].astype(np.int64)) >= 0).all(), "time went back"
     node = tr[(tr["cls"] <= 1) & (tr["node"] < 8)]  # node events (messages, timers)
@@ -90,13 +112,15 @@ CASES = [("figure_8_unreliable_2c", {}), ("figure_8_unreliable_crash", {}),
 
 @pytest.mark.parametrize("test,kw", CASES)
 def test_oracle_traces_hold_raft_properties(oracle, test, kw):
-    terms = 0
+    terms = groups = 0
     for c in range(24):
         cfg = oracle.cfg(test, **kw)
-        r, tr = oracle.run_cluster(cfg, c, trace_cap=1 << 17)
+        r, tr, dg = oracle.run_cluster_dig(cfg, c, 1 << 17)
         assert tr[-1]["cls"] == 3 and tr[-1]["kind"] == r["code"], "trace truncated"
         terms += check_trace(tr, test, int(cfg.n_nodes))
+        groups += check_apply_digests(tr, dg)
     assert terms > 24  # leaders were elected: the properties had something to hold for
+    assert groups > 24  # applied prefixes were compared by value
 
 
 @pytest.mark.gpu
@@ -109,9 +133,11 @@ def test_gpu_traces_hold_raft_properties(hip, test, kw):
     with hip.Batch(test, 64, trace_clusters=16, trace_cap=1 << 17, **kw) as b:
         b.run()
         traces = [b.trace(k) for k in range(16)]
+        digests = [b.trace_digests(k) for k in range(16)]
         n = int(b.cfg.n_nodes)
     assert all(tr[-1]["cls"] == 3 for tr in traces)  # complete: each ends with its verdict
     assert sum(check_trace(tr, test, n) for tr in traces) > 16
+    assert sum(check_apply_digests(tr, dg) for tr, dg in zip(traces, digests)) > 16
 
 
 @pytest.mark.gpu
@@ -124,16 +150,18 @@ def test_gpu_traces_hold_raft_properties(hip, test, kw):
 def test_gpu_traces_at_baseline_size(hip, test, clusters, kw):
     """The same properties on traces taken from a BASELINE-size run: 48 clusters spread over
     the batch (cluster_base shards of the full job, each traced whole) keep every property."""
-    terms = 0
+    terms = groups = 0
     for first in (0, clusters // 2, clusters - 16):
         with hip.Batch(test, 16 if first else clusters, cluster_base=first, trace_clusters=16,
                        trace_cap=1 << 17, **kw) as b:
             b.run()
             traces = [b.trace(k) for k in range(16)]
+            digests = [b.trace_digests(k) for k in range(16)]
             n = int(b.cfg.n_nodes)
         assert all(tr[-1]["cls"] == 3 for tr in traces)
         terms += sum(check_trace(tr, test, n) for tr in traces)
-    assert terms > 48
+        groups += sum(check_apply_digests(tr, dg) for tr, dg in zip(traces, digests))
+    assert terms > 48 and groups > 48
 
 
 @pytest.mark.parametrize("test,bug,check,floor", [
@@ -157,4 +185,43 @@ def test_trace_properties_catch_buggy_raft(oracle, test, bug, check, floor):
                 check_trace(tr, test, int(cfg.n_nodes))
         except AssertionError:
             caught += 1
+    assert caught >= floor
+
+
+# floors: the counts over 64 seeds when written (64 / 61 / 64), rounded down
+@pytest.mark.parametrize("test,bug,floor", [
+    ("figure_8_unreliable_2c", _abi.MR_F_BUG_NO_PREV_CHECK, 50),
+    ("figure_8_unreliable_2c", _abi.MR_F_BUG_VOTE_STALE, 45),
+    ("rejoin_2b", _abi.MR_F_BUG_NO_PREV_CHECK, 40)])
+def test_apply_digests_catch_diverging_state_machines(oracle, test, bug, floor):
+    """check_apply_digests is not vacuous: with the tester's own value check off
+    (MR_F_BUG_NO_APPLY_CHECK, so the run is not stopped at the first APPLY_MISMATCH), a Raft
+    without the prevLogTerm check (or voting for stale logs) applies different commands at the
+    same index on other nodes, and the digests in the trace alone show it."""
+    caught = 0
+    for c in range(64):
+        cfg = oracle.cfg(test, flags=bug | _abi.MR_F_BUG_NO_APPLY_CHECK)
+        _, tr, dg = oracle.run_cluster_dig(cfg, c, 1 << 17)
+        try:
+            check_apply_digests(tr, dg)
+        except AssertionError:
+            caught += 1
+    assert caught >= floor
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("test,bug,floor", [
+    ("figure_8_unreliable_2c", _abi.MR_F_BUG_NO_PREV_CHECK, 50),
+    ("rejoin_2b", _abi.MR_F_BUG_NO_PREV_CHECK, 40)])
+def test_gpu_apply_digests_catch_diverging_state_machines(hip, test, bug, floor):
+    """The same on the HIP path's own traces and digests (no oracle in the loop)."""
+    with hip.Batch(test, 64, trace_clusters=64, trace_cap=1 << 17,
+                   flags=bug | _abi.MR_F_BUG_NO_APPLY_CHECK) as b:
+        b.run()
+        caught = 0
+        for k in range(64):
+            try:
+                check_apply_digests(b.trace(k), b.trace_digests(k))
+            except AssertionError:
+                caught += 1
     assert caught >= floor
