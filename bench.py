@@ -204,6 +204,7 @@ def main():
                   safety=not a.no_safety)
     n = int(b.cfg.n_nodes)
     elapsed, acc = time_steps(b, _abi.README_SEED, total, a.warmup, a.steps, barrier)
+    kernel = b.kernel  # mr_batch_kernel: the kernel the timed launches ran
     b.close()
     r0 = summed(acc)
     last = acc[-1][1]
@@ -215,7 +216,7 @@ def main():
         tot.update({k: red[k] for k in r0 if k in red})
         last = red
     seeds = total * a.steps
-    # roofline of the dominant kernel (step_kernel): this rank's algorithmic bytes over its
+    # roofline of the dominant kernel (pool_kernel / step_kernel): this rank's algorithmic bytes over its
     # timed launches / their summed HIP-event durations (events recorded on the batch's own
     # stream around every launch; rocprofv3 --kernel-trace agrees, profiles/)
     r0_bytes = alg_bytes(r0, n)
@@ -259,7 +260,7 @@ def main():
                                               if pmc and "sq_insts_valu_per_launch" in pmc else None),
                      "traffic_source": (f"{pmc['file']} (lib {lib_sha}): {pmc.get('method', '')}"
                                         if pmc else f"no PMC record of lib {lib_sha} on this workload"),
-                     "kernel": "step_kernel",
+                     "kernel": kernel,
                      "launches": r0["launches"],
                      "avg_launch_ms": round(r0["kernel_ms"] / max(r0["launches"], 1), 4),
                      "alg_bytes_per_launch": round(per_launch),

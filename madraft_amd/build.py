@@ -97,6 +97,8 @@ def _units(csrc, scns=None, tape=True):
                                            f"-DMR_SCN_LIST=MR_INST({i})", "-DMR_NB=8",
                                            "-DMR_MW=4"]))
     host = ["-DMR_DEV_SCNS=" + " ".join(f"MR_INST({i})" for i in scns)] if scns else []
+    if not tape:
+        host.append("-DMR_NO_TAPE=1")
     for src in sorted(glob.glob(os.path.join(csrc, "*.cpp"))):
         units.append((src, os.path.splitext(os.path.basename(src))[0], host))
     return units

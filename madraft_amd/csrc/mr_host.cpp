@@ -20,7 +20,11 @@ namespace mr {
 // (mr_dev.h has_exact), else the generic 8-server one
 template <uint32_t S>
 static hipError_t launch_any(const Dev& D, uint32_t budget, hipStream_t s) {
+#if MR_NO_TAPE  // a debug library without decision-tape kernels (build.build_guard)
+  if (D.tape_mode) return hipErrorInvalidValue;
+#else
   if (D.tape_mode) return launch_step_tape_t<S, MR_MAX_NODES>(D, budget, s);
+#endif
   if (D.pool) {  // the pool kernel (mr_dev.h has_pool; the host sets D.pool only where it exists)
     if constexpr (has_pool(S, 3)) if (D.n == 3) return launch_pool_t<S, 3>(D, budget, s);
     if constexpr (has_pool(S, 5)) if (D.n == 5) return launch_pool_t<S, 5>(D, budget, s);

@@ -30,6 +30,8 @@ ONE_NO_AGREEMENT = 6  # include/madraft_sim.h MR_FAIL_ONE_NO_AGREEMENT (tester.r
 
 def make_cfg(o, a):
     kw = {"flags": _abi.MR_F_UNRELIABLE} if a.unreliable else {}
+    if a.seed_offset:  # tools/configs.py times seeds README_SEED + 2 * clusters + [0, clusters)
+        kw["seed_base"] = _abi.README_SEED + a.seed_offset
     if a.nodes:
         kw["n_nodes"] = a.nodes
         if a.nodes > 5:  # as madraft_amd.sim.make_cfg: 7-node runs keep 64 message slots
@@ -118,10 +120,13 @@ def main():
     ap.add_argument("nodes", type=int, nargs="?", default=0)
     ap.add_argument("--unreliable", action="store_true")
     ap.add_argument("--explain", type=int, default=0)
+    ap.add_argument("--seed-offset", type=int, default=0,
+                    help="seed_base = README_SEED + this (the configs table's range: 2 x clusters)")
     a = ap.parse_args()
     code, t = scan(a)
     h = collections.Counter(code.tolist())
-    print(f"{a.test} nodes={a.nodes or 'default'} unreliable={a.unreliable} clusters={a.clusters}: "
+    print(f"{a.test} nodes={a.nodes or 'default'} unreliable={a.unreliable} clusters={a.clusters} "
+          f"seed_base=README_SEED+{a.seed_offset}: "
           f"verdicts {dict(sorted(h.items()))}")
     bad = np.nonzero(code != 0)[0]
     print(f"failing clusters (first 40): {bad[:40].tolist()}")

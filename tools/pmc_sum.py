@@ -1,4 +1,4 @@
-"""Summarise rocprofv3 --pmc passes (tools/pmc.sh output) for step_kernel.
+"""Summarise rocprofv3 --pmc passes (tools/pmc.sh output) for pool_kernel / step_kernel.
 
 usage: python tools/pmc_sum.py <pmc_dir> [--json out.json --test T --clusters C]
 
@@ -26,11 +26,13 @@ a = ap.parse_args()
 
 agg = collections.defaultdict(float)
 disp = {}
+kernels = set()
 for p in sorted(glob.glob(f"{a.dir}/p*/run_counter_collection.csv")):
     ids, names = set(), set()
     for r in csv.DictReader(open(p)):
         if "step_kernel" not in r["Kernel_Name"] and "pool_kernel" not in r["Kernel_Name"]:
             continue
+        kernels.add("pool_kernel" if "pool_kernel" in r["Kernel_Name"] else "step_kernel")
         agg[r["Counter_Name"]] += float(r["Counter_Value"])
         ids.add(r["Dispatch_Id"])
         names.add(r["Counter_Name"])
@@ -62,7 +64,8 @@ def per_launch(name):
     return agg[name] / max(disp.get(name, nd), 1)
 
 
-out = {"test": a.test, "clusters": a.clusters, "kernel": "step_kernel", "abi": 3, "lib_sha16": lib,
+kernel = "/".join(sorted(kernels))
+out = {"test": a.test, "clusters": a.clusters, "kernel": kernel, "abi": 4, "lib_sha16": lib,
        "counters": dict(agg), "dispatches": disp}
 if "FETCH_SIZE" in agg and "WRITE_SIZE" in agg:
     fs = 2 * per_launch("FETCH_SIZE") * 1024 + per_launch("WRITE_SIZE") * 1024
