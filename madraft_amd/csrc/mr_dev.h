@@ -64,10 +64,9 @@ enum : uint32_t {
 // C64_FREE1..3: free-slot mask words 1..3 (slots 64..255, MR_MW = 4 units)
 enum : uint32_t { C64_FREE, C64_DIGEST, C64_MMIN, C64_TV, C64_FREE1 = C64_TV + T_NV,
                   C64__N = C64_FREE1 + 3 };
-// Cluster scalars: cluster-minor matrices [field][C] (the default: a wave's lanes read 64
-// consecutive words of one field), or, with MR_CS_MAJOR=1 (an A/B option, measured -5 %),
-// cluster-major records cs32[c][CS_STRIDE] / cs64[c][C64_STRIDE]. The host reads rows through
-// these index macros.
+// Cluster scalars: cluster-minor matrices [field][C] (a wave's lanes read 64 consecutive words
+// of one field; cluster-major records measured -5 % in round 4). The strides pad the field
+// counts; the host reads rows through these index macros.
 constexpr uint32_t CS_STRIDE = (CS__N + 3u) & ~3u, C64_STRIDE = (C64__N + 1u) & ~1u;
 #define CS_IDX(f, c, C) ((size_t)(f) * (C) + (c))
 #define C64_IDX(f, c, C) ((size_t)(f) * (C) + (c))
