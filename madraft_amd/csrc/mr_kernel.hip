@@ -772,20 +772,8 @@ DI Dev dev_launder(const Dev& D0) {
   return D;
 }
 
-// the applier's first entries loaded early: an AppendEntries request issues them with its probe,
-// so the applier does not start with a round trip of its own. Entries i0 .. i0 + N - 1 with their
-// checker records, valid up to index hi (the request rewrites no index <= prev). N = AC_APPLY
-// for the KV servers' node_apply, 1 for node_apply_coop (a follower's commit mostly moves by one)
-template <uint32_t N>
-struct ApPre {
-  LE e[N];
-  uint32_t m[N];
-  uint64_t sv[N];
-  uint32_t i0, hi;
-};
-
 template <uint32_t S>
-DI void node_apply(const Dev& D, X& x, uint32_t me, NC& d, uint32_t& kvready, const ApPre<AC_APPLY>& pre) {
+DI void node_apply(const Dev& D, X& x, uint32_t me, NC& d, uint32_t& kvready) {
   constexpr bool KV = is_svc(S);
   const bool snapmode = (x.netmode >> 1) & 1u;
   SE* const sb = D.stor + (size_t)x.c * D.apply_cap;
@@ -809,15 +797,7 @@ DI void node_apply(const Dev& D, X& x, uint32_t me, NC& d, uint32_t& kvready, co
       sv[j] = s.val;
     }
   };
-  if (d.applied < d.commit) {
-    const uint32_t top = d.commit < d.applied + AC_APPLY ? d.commit : d.applied + AC_APPLY;
-    if (pre.i0 == d.applied + 1u && top <= pre.hi) {
-#pragma unroll
-      for (uint32_t j = 0; j < AC_APPLY; j++) { e[j] = pre.e[j]; m[j] = pre.m[j]; sv[j] = pre.sv[j]; }
-    } else {
-      load_batch(d.applied + 1);
-    }
-  }
+  if (d.applied < d.commit) load_batch(d.applied + 1);
   while (d.applied < d.commit) {
     const uint32_t i0 = d.applied + 1;
     LE ce[AC_APPLY];
@@ -892,7 +872,7 @@ DI void node_apply(const Dev& D, X& x, uint32_t me, NC& d, uint32_t& kvready, co
 // Helper work is found by a wave-uniform loop over the owning lanes (readlane), so lanes
 // that are not in this call never contribute a value.
 template <uint32_t S>
-DI void node_apply_coop(const Dev& D, X& x, uint32_t me, NC& d, const ApPre<1>& pre) {
+DI void node_apply_coop(const Dev& D, X& x, uint32_t me, NC& d) {
   // snap_common (the 2D tests, uses_service_snapshots) runs with service snapshots:
   // t_new(snapshot = true) precedes every node event of such a batch, so the mode is the same
   // for every lane here. A scenario whose runtime mode (x.netmode bit 1, what node_apply
@@ -916,46 +896,35 @@ DI void node_apply_coop(const Dev& D, X& x, uint32_t me, NC& d, const ApPre<1>& 
   bool anyfail = false;
   for (uint64_t m = own; m; m &= m - 1ull)
     total += (uint32_t)__builtin_amdgcn_readlane((int)cnt, (int)__builtin_ctzll(m));
-  // every owner applies one entry (a follower's commit moving by one): each applies its own, from
-  // the entry its AppendEntries request loaded early where it did
-  const bool solo = __ballot(cnt > 1u) == 0ull;
   for (uint32_t w0 = 0; w0 < total; w0 += nh) {
     // this lane's item w0 + rank: its owner lane o, index i, and o's cluster / node / length
     const uint32_t w = w0 + rank;
     uint32_t o = 64u, i = 0, oc = 0, ome = 0, olen = 0, obase = 0, oend = 0;
-    if (solo) {
-      if (cnt) { o = lane; i = base; obase = base; oend = base; oc = x.c; ome = me; olen = len0; }
-    } else {
-      uint32_t pre_n = 0;
-      for (uint64_t m = own; m; m &= m - 1ull) {
-        const int ol = __builtin_ctzll(m);
-        const uint32_t oc_n = (uint32_t)__builtin_amdgcn_readlane((int)cnt, ol);
-        if (pre_n < w0 + nh && pre_n + oc_n > w0) {  // owner's range meets this round (uniform)
-          const uint32_t ob = (uint32_t)__builtin_amdgcn_readlane((int)base, ol);
-          if (w >= pre_n && w < pre_n + oc_n) {
-            o = (uint32_t)ol;
-            i = ob + (w - pre_n);
-            obase = ob;
-            oend = ob + oc_n - 1u;
-            oc = (uint32_t)__builtin_amdgcn_readlane((int)x.c, ol);
-            ome = (uint32_t)__builtin_amdgcn_readlane((int)me, ol);
-            olen = (uint32_t)__builtin_amdgcn_readlane((int)len0, ol);
-          }
+    uint32_t pre = 0;
+    for (uint64_t m = own; m; m &= m - 1ull) {
+      const int ol = __builtin_ctzll(m);
+      const uint32_t oc_n = (uint32_t)__builtin_amdgcn_readlane((int)cnt, ol);
+      if (pre < w0 + nh && pre + oc_n > w0) {  // owner's range meets this round (uniform)
+        const uint32_t ob = (uint32_t)__builtin_amdgcn_readlane((int)base, ol);
+        if (w >= pre && w < pre + oc_n) {
+          o = (uint32_t)ol;
+          i = ob + (w - pre);
+          obase = ob;
+          oend = ob + oc_n - 1u;
+          oc = (uint32_t)__builtin_amdgcn_readlane((int)x.c, ol);
+          ome = (uint32_t)__builtin_amdgcn_readlane((int)me, ol);
+          olen = (uint32_t)__builtin_amdgcn_readlane((int)len0, ol);
         }
-        pre_n += oc_n;
-        if (pre_n >= w0 + nh) break;
       }
+      pre += oc_n;
+      if (pre >= w0 + nh) break;
     }
     const bool mine = o < 64u;
     // phase 1: loads and checks (node_apply's order: capacity, count, mismatch, out of order)
     LE e = LE{};
     SE s = SE{};
     const bool inb = mine && i < D.apply_cap;
-    if (solo && inb && pre.i0 == i && i <= pre.hi) {
-      e = pre.e[0];
-      s.mask = pre.m[0];
-      s.val = pre.sv[0];
-    } else if (inb) {
+    if (inb) {
       e = D.log[((size_t)oc * D.n + ome) * D.log_cap + (i & (D.log_cap - 1u))];
       s = D.stor[(size_t)oc * D.apply_cap + GI(i, D.apply_cap, G_STOR)];
     }
@@ -1296,8 +1265,6 @@ DI void node_event(const Dev& Darg, X& x, bool is_msg, uint32_t tnode, uint32_t 
   constexpr bool KV = is_svc(S);  // kvraft / shard_ctrler request path
   uint32_t me = tnode, src = 0, type = 0, inc = 0, k = 0, mterm = 0, ma = 0, mb = 0, mc = 0;
   uint32_t kvready = 0;  // KV: the pending-request slots answered in this event (kv_flush)
-  ApPre<KV ? AC_APPLY : 1u> pre;  // the applier's first entries, if an AppendEntries request loaded them
-  pre.i0 = 0u; pre.hi = 0u;
   uint32_t hdr_bits = 0;
   // the server is known from the event key, so its record, next[] / match[] and pending
   // payload range are loaded together with the message (a clerk host has no record)
@@ -1447,23 +1414,6 @@ DI void node_event(const Dev& Darg, X& x, bool is_msg, uint32_t tnode, uint32_t 
         uint32_t lt[AC], ors[AC];
         uint64_t ov[AC];
         const uint32_t lrs = LRS(me);
-        {  // the commit this request brings: the applier's first entries with the probe
-          const uint32_t lc0 = mc < ma + k ? mc : ma + k, hi = ma < d.last ? ma : d.last;
-          if (lc0 > d.applied && d.applied < hi) {
-            const SE* sb = D.stor + (size_t)x.c * D.apply_cap;
-            pre.i0 = d.applied + 1u;
-            pre.hi = hi;
-#pragma unroll
-            for (uint32_t j = 0; j < (KV ? AC_APPLY : 1u); j++) {
-              const uint32_t i = pre.i0 + j;
-              const bool ok = i <= hi && i < D.apply_cap;
-              pre.e[j] = ok ? D.log[logi(D, x, me, i)] : LE{};
-              const SE sj = ok ? sb[i] : SE{};
-              pre.m[j] = sj.mask;
-              pre.sv[j] = sj.val;
-            }
-          }
-        }
         uint32_t tp, rsp;  // term and run start of our entry at prev
         le_at(D, x, me, d, lrs, prev, tp, rsp);
         ae_load_batch(D, x, me, d, src, mat, pp, ma, k, j0, pe, lt, ov, ors);
@@ -1615,18 +1565,16 @@ DI void node_event(const Dev& Darg, X& x, bool is_msg, uint32_t tnode, uint32_t 
     rawt[p] = (mode == SEND_APPEND && bit(peers & reach, p) && p < D.n && ix != 0u && need)
                   ? D.log[logi(D, x, me, ix)].term : 0u;
   }
-  if constexpr (!KV && kv_gen(S).maxraft == 0) {
+  if (!KV && kv_gen(S).maxraft == 0) {
     if (__ballot(d.applied < d.commit)) {  // committed entries reach the tester's applier
-      node_apply_coop<S>(D, x, me, d, pre);
+      node_apply_coop<S>(D, x, me, d);
       if (x.code != RUN) return;
       PROF(P_APPLY);
     }
-  } else {
-    if (d.applied < d.commit) {
-      node_apply<S>(D, x, me, d, kvready, pre);
-      if (x.code != RUN) return;
-      PROF(P_APPLY);
-    }
+  } else if (d.applied < d.commit) {
+    node_apply<S>(D, x, me, d, kvready);
+    if (x.code != RUN) return;
+    PROF(P_APPLY);
   }
   if (mode == SEND_REPLY) peers = 1u << src;
   const uint32_t lt = mode == SEND_VOTE ? d.lastt : 0u;  // term_at(last)
