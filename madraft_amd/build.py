@@ -50,11 +50,15 @@ def has_exact(i, nb):
 
 # Raft-only test bodies without spawned threads (mr_dev.h has_pool): the pool-kernel instances
 POOL_SCNS = set(range(1, 15)) | {16} | set(range(19, 25))
+# the kvraft / shard_ctrler test bodies (mr_dev.h is_svc): the service pool (MR_POOL=2), all but
+# the 20-clerk snapshot_recover_many_clients_3b (256 message slots)
+SVC_SCNS = set(range(25, 48))
+SVC_POOL_SCNS = SVC_SCNS - WIDE_SLOTS
 
 
 def has_pool(i, nb):
     """mr_dev.h has_pool: a pool-kernel instance of scenario i at nb servers is built."""
-    return nb <= 5 and has_exact(i, nb) and i in POOL_SCNS
+    return has_exact(i, nb) and ((nb <= 5 and i in POOL_SCNS) or i in SVC_POOL_SCNS)
 
 
 def _units(csrc, scns=None, tape=True):
@@ -77,13 +81,16 @@ def _units(csrc, scns=None, tape=True):
         for i in wide:  # 256 message slots (mr_kernel.hip MR_MW)
             units.append((kern, f"nb{nb}_w{i}", ["-DMR_COMMON=0", f"-DMR_SCN_LIST=MR_INST({i})",
                                                  f"-DMR_NB={nb}", "-DMR_MW=4", *key]))
-    for nb in (3, 5):  # pool kernels: 32-bit keys
-        ids = [i for i in (scns or SCN_IDS) if has_pool(i, nb)]
-        ng = max(1, min(N_GROUPS, (len(ids) + 2) // 3)) if ids else 0
-        for g in range(ng):
-            lst = " ".join(f"MR_INST({i})" for i in ids[g::ng])
-            units.append((kern, f"pool{nb}_{g}", ["-DMR_COMMON=0", f"-DMR_SCN_LIST={lst}",
-                                                  f"-DMR_NB={nb}", "-DMR_KEY32=1", "-DMR_POOL=1"]))
+    for nb in (3, 5, 7):  # pool kernels: 32-bit keys; Raft-only / service
+        for kind, pool in (("pool", 1), ("svcpool", 2)):
+            ids = [i for i in (scns or SCN_IDS)
+                   if has_pool(i, nb) and (i in SVC_POOL_SCNS) == (pool == 2)]
+            ng = max(1, min(N_GROUPS, (len(ids) + 2) // 3)) if ids else 0
+            for g in range(ng):
+                lst = " ".join(f"MR_INST({i})" for i in ids[g::ng])
+                units.append((kern, f"{kind}{nb}_{g}", ["-DMR_COMMON=0", f"-DMR_SCN_LIST={lst}",
+                                                        f"-DMR_NB={nb}", "-DMR_KEY32=1",
+                                                        f"-DMR_POOL={pool}"]))
     ids = list(scns or SCN_IDS) if tape else []  # decision-tape builds (SEMANTICS §12), NB = 8
     wide = [i for i in ids if i in WIDE_SLOTS]
     ids = [i for i in ids if i not in WIDE_SLOTS]

@@ -314,12 +314,16 @@ constexpr bool has_exact(uint32_t s, uint32_t n) {
                     (has_nb7(s) && n == 7u));
 }
 // pool-kernel instances (mr_kernel.hip pool_kernel): Raft-only test bodies
-// without spawned threads, at an exact server count of 3 or 5 (up to 32 message slots: the
-// 32-bit keys of a 512-cluster pool take 64 KiB of LDS)
+// without spawned threads at an exact server count of 3 or 5 (512-cluster pools, up to 32
+// message slots: their 32-bit keys take 64 KiB of LDS), and the kvraft / shard_ctrler test
+// bodies at their exact server count (256-cluster pools, up to 64 message slots; not the
+// 20-clerk snapshot_recover_many_clients_3b, whose 256 slots and clerk hosts do not fit)
 constexpr bool has_pool(uint32_t s, uint32_t n) {
-  return n <= 5u && has_exact(s, n) && !is_svc(s) && nthr(s) == 0;
+  return has_exact(s, n) &&
+         ((n <= 5u && !is_svc(s) && nthr(s) == 0) ||
+          (is_svc(s) && s != MR_SCN_KV_SNAPSHOT_RECOVER_MANY_CLIENTS_3B));
 }
-constexpr uint32_t POOL_MAX_SLOTS = 32;
+constexpr uint32_t pool_max_slots(uint32_t s) { return is_svc(s) ? 64u : 32u; }
 // scenarios whose test body starts the tester with service snapshots (t_new(snapshot = true),
 // tester.rs:303-325 SNAPSHOT_INTERVAL): snap_common's five 2D tests. node_apply_coop specializes
 // on it at compile time and checks it against the runtime mode (x.netmode bit 1).

@@ -28,6 +28,7 @@ static hipError_t launch_any(const Dev& D, uint32_t budget, hipStream_t s) {
   if (D.pool) {  // the pool kernel (mr_dev.h has_pool; the host sets D.pool only where it exists)
     if constexpr (has_pool(S, 3)) if (D.n == 3) return launch_pool_t<S, 3>(D, budget, s);
     if constexpr (has_pool(S, 5)) if (D.n == 5) return launch_pool_t<S, 5>(D, budget, s);
+    if constexpr (has_pool(S, 7)) if (D.n == 7) return launch_pool_t<S, 7>(D, budget, s);
     return hipErrorInvalidValue;
   }
   if constexpr (has_exact(S, 3)) if (D.n == 3) return launch_step_t<S, 3>(D, budget, s);
@@ -40,6 +41,7 @@ static uint32_t capacity_any(const Dev& D, int device) {
   if (D.pool) {
     if constexpr (has_pool(S, 3)) if (D.n == 3) return pool_capacity_t<S, 3>(device, D.M);
     if constexpr (has_pool(S, 5)) if (D.n == 5) return pool_capacity_t<S, 5>(device, D.M);
+    if constexpr (has_pool(S, 7)) if (D.n == 7) return pool_capacity_t<S, 7>(device, D.M);
     return 0;
   }
   if constexpr (has_exact(S, 3)) if (D.n == 3) return step_capacity_t<S, 3>(device, D.M);
@@ -75,14 +77,13 @@ static uint32_t step_capacity(const Dev& D, uint32_t scn, int device) {
     default: return 0;
   }
 }
-// the pool kernel serves this batch: an instance exists, the key rows fit (M <= 32), and the
+// the pool kernel serves this batch: an instance exists, the key rows fit (pool_max_slots), and the
 // environment does not turn it off (MR_POOL=0: the per-lane step kernel, for A/B runs)
 static bool use_pool(uint32_t scn, uint32_t n, uint32_t M) {
-  if (M > POOL_MAX_SLOTS) return false;
   if (const char* e = std::getenv("MR_POOL")) if (e[0] == '0') return false;
   switch (scn) {
 #define MR_INST(S) \
-  case S: return has_pool(S, n);
+  case S: return has_pool(S, n) && M <= pool_max_slots(S);
 #ifdef MR_DEV_SCNS
     MR_DEV_SCNS
 #else

@@ -68,6 +68,7 @@ struct X {
   uint32_t timer[NB];  // node timers (election / heartbeat deadline), INF_T = none
   uint32_t cnt[CNT__N];  // pool_kernel: the lane's sums over its events (per cluster: POOL_CNT)
   uint32_t ls;  // pool_kernel: the cluster's pool slot (its LDS column)
+  uint64_t aem;  // pool_kernel (MR_POOL 2): the message slots that hold AppendEntries requests
 };
 
 // MR_GUARD (a debug build, build.build_guard; tests/test_guard.py): every computed index into a
@@ -136,7 +137,9 @@ constexpr uint32_t AE_OTHERS = 32;
 #define MR_POOL 0
 #endif
 static_assert(!MR_POOL || MR_KEY32, "the pool kernel keeps 32-bit message keys");
-constexpr uint32_t POOL_WAVES = 8, POOL_SLOTS = 64 * POOL_WAVES;
+// MR_POOL 1: the Raft-only pool (8 waves, 512 clusters); 2: the kvraft / shard_ctrler pool (4 waves
+// of 256 clusters: their 64 message slots' keys and one wave per SIMD of registers)
+constexpr uint32_t POOL_WAVES = MR_POOL == 2 ? 4 : 8, POOL_SLOTS = 64 * POOL_WAVES;
 using lkey_t = std::conditional_t<MR_KEY32 != 0, uint32_t, uint64_t>;
 constexpr lkey_t LKEY_FREE = ~lkey_t(0);
 constexpr uint32_t T_KEY_MAX = (1u << 27) - 1u;  // delivery times at or past it: SIM_CAPACITY
@@ -608,12 +611,16 @@ DI int net_send(const Dev& D, X& x, uint32_t src, uint32_t& nctr, uint32_t dst, 
   x.inflight++;
   CMAX(CNT_MAX_INFLIGHT, x.inflight);
   if constexpr (MR_KEY32) {
-    // pool kernels (Raft-only, dst < 8): bit 3 marks an AppendEntries request, the event kind
-    // the pool bins by (pool_kind); dst is key & 7 there
-    const uint32_t lo = !MR_POOL ? dst
+    // Raft-only pool kernels (dst < 8): bit 3 marks an AppendEntries request, bit 4 a
+    // RequestVote, the event kinds the pool bins by (pool_kind); dst is key & 7 there. The
+    // service pool keeps dst (clerk hosts up to 8 + 16) and marks AppendEntries slots in x.aem
+    const uint32_t lo = MR_POOL != 1 ? dst
                         : type == M_AE_REQ ? dst | 8u
                         : type == M_RV_REQ || type == M_RV_REP ? dst | 16u
                                                                : dst;
+    if constexpr (MR_POOL == 2) {
+      if (type == M_AE_REQ) x.aem |= 1ull << slot;
+    }
     LK(slot) = (t << 5) | lo;
     // every message in flight has a smaller seq: a new one is earliest only by time
     if (t < (uint32_t)(x.mmin >> 32)) { x.mmin = ((uint64_t)t << 32) | lo; x.mslot = slot; }
@@ -1292,6 +1299,7 @@ DI void node_event(const Dev& Darg, X& x, bool is_msg, uint32_t tnode, uint32_t 
     LK(slot) = LKEY_FREE;
     if constexpr (MW == 1) {
       x.free_mask[0] |= 1ull << slot;
+      if constexpr (MR_POOL == 2) x.aem &= ~(1ull << slot);
     } else {
 #pragma unroll
       for (uint32_t w = 0; w < MW; w++) x.free_mask[w] |= (slot >> 6) == w ? 1ull << (slot & 63u) : 0ull;

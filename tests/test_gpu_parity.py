@@ -391,3 +391,23 @@ def test_golden_fixtures_on_gpu(hip):
         assert t.tolist() == case["time_us"], case["test"]
         assert [format(int(d), "016x") for d in dig] == case["digest"], case["test"]
         assert ev == case["events"], case["test"]
+
+
+@pytest.mark.parametrize("test", ["unreliable_3a", "persist_partition_unreliable_linearizable_3a",
+                                  "basic_4a", "figure_8_unreliable_2c"])
+def test_pool_and_step_kernels_agree(hip, monkeypatch, test):
+    """The pool kernel (Raft-only bodies and, round 5, the kvraft / shard_ctrler ones) and the
+    per-lane step kernel (MR_POOL=0) give the same verdicts, times, digests and counters: only
+    which lanes run together differs."""
+    def run():
+        with hip.Batch(test, 256) as b:
+            b.run()
+            return b.kernel, b.verdicts(), b.counters()
+    kp, vp, cp = run()
+    monkeypatch.setenv("MR_POOL", "0")
+    ks, vs, cs = run()
+    assert (kp, ks) == ("pool_kernel", "step_kernel")
+    for a, c in zip(vp, vs):
+        assert np.array_equal(a, c)
+    for k in COUNTER_KEYS:
+        assert cp[k] == cs[k], k

@@ -19,6 +19,7 @@ CONFIGS = {
     "C4": ("snapshot_install_unreliable_2d", 262144, dict(nodes=7)),
     "C5": ("unreliable_3a", 65536, {}),
     "C5L": ("persist_partition_unreliable_linearizable_3a", 65536, {}),
+    "C5L3b": ("snapshot_unreliable_recover_concurrent_partition_linearizable_3b", 65536, {}),
 }
 tag = sys.argv[1]
 names = sys.argv[2].split(",") if len(sys.argv) > 2 else list(CONFIGS)
