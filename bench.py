@@ -168,7 +168,7 @@ def main():
     ap.add_argument("--variant-steps", type=int, default=2)
     ap.add_argument("--million", type=int, default=1 << 20,
                     help="N = 1 only: config 3's whole job (this many clusters) of the headline test and "
-                         "of its crash variant, each on this one GPU as consecutive resident chunks "
+                         "of its crash variant, each on this one GPU streaming through the resident pools "
                          "(0 = skip)")
     ap.add_argument("--cpu-seeds", type=int, default=320000,
                     help="cpu_baseline sample: seeds in total, split over one process per core")
@@ -306,7 +306,7 @@ def main():
                 "ms_per_job": round(em * 1000, 3), "events_per_sec": round(sm["events"] / em, 1),
                 "events_per_seed": round(sm["events"] / a.million, 1),
                 "pass_rate": round(sm["passed"] / max(sm["done"], 1), 6), "launches": sm["launches"],
-                "note": "config 3's whole job on one MI355X (consecutive resident chunks)"}
+                "note": "config 3's whole job on one MI355X (streaming through the resident pools)"}
     if world == 1 and not a.no_cpu_baseline:  # N = 1 only: the N > 1 lines are scaling points
         # one process per host core this job may use (north_star): the CPUs it may run on, capped
         # by its cgroup CPU quota — on the GPU box 256 CPUs are visible but the quota is 16

@@ -398,14 +398,6 @@ static int mr_batch_create_impl(const mr_cfg* cfg, mr_batch** out) {
     *it.p = it.bytes ? p : nullptr;
     p += (it.bytes + 255) & ~size_t(255);
   }
-  if (b->D.stream) {  // held-cluster lists, L entries each (L <= C)
-    e = hipMalloc(&b->held[0], (size_t)b->D.C * sizeof(uint32_t));
-    if (e == hipSuccess) e = hipMalloc(&b->held[1], (size_t)b->D.C * sizeof(uint32_t));
-    if (e != hipSuccess) {
-      mr_batch_destroy(b);
-      return set_err(std::string("held-list allocation failed: ") + hipGetErrorString(e));
-    }
-  }
   if (cfg->flags & MR_F_RECORD) {
     e = hipMalloc(&b->tape, (size_t)C * cfg->tape_cap * sizeof(uint4));
     if (e != hipSuccess) {
@@ -429,7 +421,20 @@ static int mr_batch_create_impl(const mr_cfg* cfg, mr_batch** out) {
              : (cap && (uint64_t)(cfg->lanes && cfg->lanes < C ? cfg->lanes : C) * 2u <= cap) ? 32u : 64u;
   if (!cfg->lanes) {  // a batch bigger than the resident waves runs as chunks of that size
     const uint32_t capc = (uint32_t)((uint64_t)cap * b->D.lpw / STEP_LANES);
-    if (capc && capc < b->D.C) b->D.L = capc;
+    if (capc && capc < b->D.C) {
+      b->D.L = capc;
+      // a pool kernel refills its slots from the rest of the batch (streaming) instead of
+      // draining once per chunk (config 3's whole job on one GPU +10 %)
+      if (b->D.pool && !b->D.tape_mode) b->D.stream = 1u;
+    }
+  }
+  if (b->D.stream) {  // held-cluster lists, L entries each (L <= C)
+    e = hipMalloc(&b->held[0], (size_t)b->D.C * sizeof(uint32_t));
+    if (e == hipSuccess) e = hipMalloc(&b->held[1], (size_t)b->D.C * sizeof(uint32_t));
+    if (e != hipSuccess) {
+      mr_batch_destroy(b);
+      return set_err(std::string("held-list allocation failed: ") + hipGetErrorString(e));
+    }
   }
   if (const char* s = std::getenv("MR_STEP_BUDGET")) b->budget = (uint32_t)std::atoi(s);
   if (b->budget == 0) b->budget = 16384;

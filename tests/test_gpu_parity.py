@@ -280,8 +280,8 @@ def test_baseline_sizes(hip, oracle, test, clusters, kw):
 def test_config3_one_million_on_one_gpu(hip, oracle, test):
     """BASELINE config 3's whole job — 1,048,576 clusters of figure_8_unreliable_2c, which the
     driver shards over 8 GPUs (131,072 each), and config 3 read literally (crash1 / start1 +
-    persister, tests.rs:612-660, in figure_8_unreliable's loop) — run on ONE MI355X as
-    consecutive chunks of the resident capacity: every cluster reaches a
+    persister, tests.rs:612-660, in figure_8_unreliable's loop) — run on ONE MI355X, streaming
+    through the resident pools: every cluster reaches a
     verdict, no simulator capacity is hit, and 64 sampled clusters equal the oracle (verdict,
     time, trace digest)."""
     n = 1 << 20

@@ -16,6 +16,8 @@ CONFIGS = {
     "C2": ("fail_agree_2b", 65536, dict(nodes=5, unreliable=True)),
     "C3": ("figure_8_unreliable_2c", 131072, dict(safety=True)),
     "C3c": ("figure_8_unreliable_crash", 131072, dict(safety=True)),
+    "C3M": ("figure_8_unreliable_2c", 1048576, dict(safety=True)),  # config 3's whole job
+    "C3cM": ("figure_8_unreliable_crash", 1048576, dict(safety=True)),
     "C4": ("snapshot_install_unreliable_2d", 262144, dict(nodes=7)),
     "C5": ("unreliable_3a", 65536, {}),
     "C5L": ("persist_partition_unreliable_linearizable_3a", 65536, {}),
