@@ -221,3 +221,47 @@ def test_gpu_kv_replay_catches_duplicate_appends(hip):
             except AssertionError:
                 caught += 1
     assert caught >= 40
+
+
+def _cmd(op, key, clerk, seq, elem):
+    """a SEMANTICS §9 log command"""
+    return (1 << 63) | (op << 61) | (key << 55) | (clerk << 48) | (seq << 24) | elem
+
+
+def _log(cmds, bad_hash_at=None):
+    """[n, 2] applies of `cmds` (indices 1..) with the hashes a correct server reports"""
+    ap = np.zeros((len(cmds) + 1, 2), np.uint64)
+    vals, ded = {}, {}
+    for i, c in enumerate(cmds, 1):
+        op, key, clerk, seq, elem = decode(c)
+        v = vals.setdefault(key, Value())
+        if op != GET and seq > ded.get(clerk, 0):
+            v.put(elem, False) if op == PUT else v.append(elem)
+            ded[clerk] = seq
+        ap[i] = (c, v.h if i != bad_hash_at else v.h ^ 1)
+    return ap
+
+
+def test_kv_replay_checker_units():
+    """The replay on hand-made logs: a generic_test client (clerk 3, key 0: Put "", Appends of
+    "x 0 j y", Gets) passes; a dropped dedup, an append out of order, a call before its
+    predecessor and a wrong server hash each fail."""
+    ok = [_cmd(PUT, 0, 3, 1, 0), _cmd(APPEND, 0, 3, 2, 0), _cmd(APPEND, 0, 3, 3, 1),
+          _cmd(APPEND, 0, 3, 3, 1),  # a retried Append: a duplicate the servers skip
+          _cmd(GET, 0, 3, 4, 0), _cmd(APPEND, 0, 3, 5, 2), _cmd(GET, 0, 3, 6, 0)]
+    assert check_kv_applies(_log(ok), False, True) == (2, 7)
+    with pytest.raises(AssertionError):  # the server reports the retried Append applied twice
+        ap = _log(ok)
+        v = Value()
+        v.put(0, False)
+        for e in (0, 1, 1):
+            v.append(e)
+        ap[4, 1] = v.h
+        check_kv_applies(ap, False, True)
+    with pytest.raises(AssertionError):  # "x 0 1 y" before "x 0 0 y"
+        check_kv_applies(_log([_cmd(PUT, 0, 3, 1, 0), _cmd(APPEND, 0, 3, 2, 1), _cmd(APPEND, 0, 3, 3, 0)]),
+                         False, True)
+    with pytest.raises(AssertionError):  # call 3 in the log before call 2
+        check_kv_applies(_log([_cmd(PUT, 0, 3, 1, 0), _cmd(APPEND, 0, 3, 3, 0)]), False, True)
+    with pytest.raises(AssertionError):  # a server hash that is not the replayed value's
+        check_kv_applies(_log(ok, bad_hash_at=5), False, True)

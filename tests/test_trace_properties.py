@@ -225,3 +225,18 @@ def test_gpu_apply_digests_catch_diverging_state_machines(hip, test, bug, floor)
             except AssertionError:
                 caught += 1
     assert caught >= floor
+
+
+def test_apply_digest_checker_units():
+    """check_apply_digests on hand-made records: equal applied indices with equal digests pass,
+    with different ones fail; invalid digests (a snapshot install / restart) are skipped."""
+    tr = np.zeros(4, _abi.EVENT_DTYPE)
+    tr["cls"] = 0
+    tr["node"] = [0, 1, 2, 1]
+    tr["applied"] = [3, 3, 5, 5]
+    d = _abi.apply_mix(1, 11) + _abi.apply_mix(2, 12) + _abi.apply_mix(3, 13)
+    dg = np.array([d & (2**64 - 1), d & (2**64 - 1), 7, _abi.DIGEST_INVALID], np.uint64)
+    assert check_apply_digests(tr, dg) == 1
+    dg[1] ^= 1
+    with pytest.raises(AssertionError):
+        check_apply_digests(tr, dg)
