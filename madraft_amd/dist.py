@@ -4,10 +4,10 @@ Clusters (seeds) are independent — there is no inter-cluster traffic in any
 in-scope test — so rank r of W owns the contiguous global
 cluster range shard(total, W, r) and runs the identical kernel on it. Seeds
 derive from global cluster ids, so results do not depend on W. The only
-collective is one all-reduce of the batch counters at the end: sum for
-counts, verdict and coverage histograms, max for maxima, min for the first failing global cluster id. With
-backend "nccl" that all-reduce is RCCL over xGMI; a few hundred bytes,
-latency-bound. Tests run the same code with gloo on CPU.
+collective is one all-gather of each rank's counter vector at the end (about 1 KB per rank),
+reduced on every rank: sum for counts, verdict and coverage histograms, max for maxima, min for
+the first failing global cluster id — one latency-bound collective instead of one per reduction
+op. With backend "nccl" it is RCCL over xGMI. Tests run the same code with gloo on CPU.
 """
 import torch
 import torch.distributed as dist
@@ -50,9 +50,15 @@ def allreduce_counters(c, device=None, group=None):
     cov = torch.tensor([int(v) for k in COV_KEYS for v in c.get(k, [0] * 16)], dtype=torch.int64,
                        device=dev)
     s = torch.cat([s, h, cov])
-    dist.all_reduce(s, op=dist.ReduceOp.SUM, group=group)
-    dist.all_reduce(m, op=dist.ReduceOp.MAX, group=group)
-    dist.all_reduce(f, op=dist.ReduceOp.MIN, group=group)
+    # one collective: every rank's [sums | maxima | first failure], reduced locally
+    v = torch.cat([s, m, f])
+    parts = [torch.empty_like(v) for _ in range(dist.get_world_size(group))]
+    dist.all_gather(parts, v, group=group)
+    g = torch.stack(parts)
+    ns, nm = s.numel(), m.numel()
+    s = g[:, :ns].sum(dim=0)
+    m = g[:, ns:ns + nm].max(dim=0).values
+    f = g[:, ns + nm:].min(dim=0).values
     out = dict(c)
     sl = s.tolist()
     out["fail_hist"] = {name: int(v) for (_, name), v in zip(names, sl[len(SUM_KEYS):]) if v}
