@@ -20,8 +20,16 @@ GUARD_SCNS = [10, 16, 17, 18] + list(range(25, 48))
 ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950")
 
 
-def _stale(out, srcs):
+def _stale(out, srcs, key=""):
+    """`out` is missing, older than a source, or was built with other options than `key`
+    (kept in `out`.flags: a library built with other -D flags is never taken for this one)."""
     if not os.path.exists(out):
+        return True
+    try:
+        with open(out + ".flags") as f:
+            if f.read() != key:
+                return True
+    except OSError:
         return True
     t = os.path.getmtime(out)
     return any(os.path.getmtime(s) > t for s in srcs)
@@ -58,7 +66,7 @@ SVC_POOL_SCNS = SVC_SCNS - WIDE_SLOTS
 
 def has_pool(i, nb):
     """mr_dev.h has_pool: a pool-kernel instance of scenario i at nb servers is built."""
-    return has_exact(i, nb) and ((nb <= 5 and i in POOL_SCNS) or i in SVC_POOL_SCNS)
+    return has_exact(i, nb) and ((nb <= 7 and i in POOL_SCNS) or i in SVC_POOL_SCNS)
 
 
 def _units(csrc, scns=None, tape=True):
@@ -120,7 +128,8 @@ def build_hip(force=False, verbose=False, extra=(), out=None, scns=None, csrc=No
     srcs = sorted(glob.glob(os.path.join(csrc, "*.hip")) + glob.glob(os.path.join(csrc, "*.cpp")))
     deps = srcs + glob.glob(os.path.join(csrc, "*.h")) + glob.glob(os.path.join(csrc, "*.inc")) + \
         [os.path.join(ROOT, "include", "madraft_sim.h"), os.path.abspath(__file__)]
-    if not force and not _stale(out, deps):
+    key = repr((list(extra), sorted(scns) if scns else None, bool(tape), os.path.abspath(csrc), ARCH))
+    if not force and not _stale(out, deps, key):
         return out
     objdir = os.path.join(HERE, "lib", "obj" + ("_" + os.path.basename(out) if out != LIB else ""))
     os.makedirs(objdir, exist_ok=True)
@@ -150,6 +159,8 @@ def build_hip(force=False, verbose=False, extra=(), out=None, scns=None, csrc=No
         print(" ".join(cmd))
     subprocess.run(cmd, check=True)
     os.replace(out + ".tmp", out)
+    with open(out + ".flags", "w") as f:
+        f.write(key)
     return out
 
 

@@ -217,6 +217,9 @@ struct Dev {
   uint32_t* kwk;    // [C][kws(nthr)][2] thread slots' {tid, wake}: the scheduler's keys, packed
   uint32_t pool;    // the batch runs on pool_kernel (has_pool): 32-bit keys with the AE bit
   uint32_t* guard;  // [4] MR_GUARD builds: an out-of-range index {tag, cluster, index, bound}
+  uint32_t gprobe;  // MR_GUARD builds, MR_GUARD_PROBE set: cluster 0's first delivery reads slot M
+  unsigned long long* pcnt;  // [CNT__N] pool_kernel: the workgroups' counter sums (64-bit; reduce adds them)
+  uint32_t krows;   // the 7-server Raft pool: message slots whose keys live in LDS (the rest in HBM)
 };
 // words-pairs per cluster of kwk: the thread slots rounded up to whole 16-B quads (two slots each;
 // slot 0 = the test body and the pad slot hold ~0, so they never win a rescan)
@@ -224,7 +227,7 @@ constexpr uint32_t kws(uint32_t nthr) { return (nthr + 1u) & ~1u; }
 // tester frame record (tester() in mr_kernel.hip): pc | helper << 24, result, locals l[0..7],
 // helper frame h[0..4], u64 argument hv — 17 words in five 16-B quads, loaded and stored whole
 constexpr uint32_t TF_Q = 5;
-constexpr uint32_t PROF_SLOTS = 96;  // 64..85: pool_kernel statistics (MR_PROF, tools/prof.py)
+constexpr uint32_t PROF_SLOTS = 96;  // 64..94: pool_kernel statistics (MR_PROF, tools/prof.py)
 // election-safety term bitmap (MR_F_SAFETY): terms 0..LED_TERMS-1; a leader elected in a
 // later term is a simulator limit (MR_FAIL_SIM_CAPACITY); figure_8 peaks at term 177
 constexpr uint32_t LED_W = 64, LED_TERMS = 32 * LED_W;
@@ -314,16 +317,17 @@ constexpr bool has_exact(uint32_t s, uint32_t n) {
                     (has_nb7(s) && n == 7u));
 }
 // pool-kernel instances (mr_kernel.hip pool_kernel): Raft-only test bodies
-// without spawned threads at an exact server count of 3 or 5 (512-cluster pools, up to 32
-// message slots: their 32-bit keys take 64 KiB of LDS), and the kvraft / shard_ctrler test
-// bodies at their exact server count (256-cluster pools, up to 64 message slots; not the
+// without spawned threads at an exact server count of 3, 5 or 7 (512-cluster pools, up to 64
+// message slots: the 32-bit keys of slots 0..31 take 64 KiB of LDS, slots 32..63 — 7-server
+// bodies, BASELINE config 4 — keep theirs in HBM), and the kvraft / shard_ctrler test bodies at
+// their exact server count (256-cluster pools, up to 64 message slots, all keys in LDS; not the
 // 20-clerk snapshot_recover_many_clients_3b, whose 256 slots and clerk hosts do not fit)
 constexpr bool has_pool(uint32_t s, uint32_t n) {
   return has_exact(s, n) &&
-         ((n <= 5u && !is_svc(s) && nthr(s) == 0) ||
+         ((n <= 7u && !is_svc(s) && nthr(s) == 0) ||
           (is_svc(s) && s != MR_SCN_KV_SNAPSHOT_RECOVER_MANY_CLIENTS_3B));
 }
-constexpr uint32_t pool_max_slots(uint32_t s) { return is_svc(s) ? 64u : 32u; }
+constexpr uint32_t pool_max_slots(uint32_t s, uint32_t n) { return is_svc(s) || n > 5u ? 64u : 32u; }
 // scenarios whose test body starts the tester with service snapshots (t_new(snapshot = true),
 // tester.rs:303-325 SNAPSHOT_INTERVAL): snap_common's five 2D tests. node_apply_coop specializes
 // on it at compile time and checks it against the runtime mode (x.netmode bit 1).

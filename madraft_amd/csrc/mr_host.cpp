@@ -83,7 +83,7 @@ static bool use_pool(uint32_t scn, uint32_t n, uint32_t M) {
   if (const char* e = std::getenv("MR_POOL")) if (e[0] == '0') return false;
   switch (scn) {
 #define MR_INST(S) \
-  case S: return has_pool(S, n) && M <= pool_max_slots(S);
+  case S: return has_pool(S, n) && M <= pool_max_slots(S, n);
 #ifdef MR_DEV_SCNS
     MR_DEV_SCNS
 #else
@@ -374,6 +374,7 @@ static int mr_batch_create_impl(const mr_cfg* cfg, mr_batch** out) {
   add(&D.remaining, 2);
   add(&D.prof, PROF_SLOTS);
   add(&D.guard, 4);
+  add(&D.pcnt, CNT__N);
   add(&D.tfr, (size_t)TF_Q * C);
   size_t total = 0;
   for (auto& it : items) total += (it.bytes + 255) & ~size_t(255);
@@ -436,6 +437,12 @@ static int mr_batch_create_impl(const mr_cfg* cfg, mr_batch** out) {
       return set_err(std::string("held-list allocation failed: ") + hipGetErrorString(e));
     }
   }
+  // the 7-server Raft pool's LDS key rows (32); MR_KEY_ROWS (tests) puts more slots' keys in HBM
+  b->D.krows = 32u;
+  if (const char* s = std::getenv("MR_KEY_ROWS")) {
+    const int r = std::atoi(s);
+    if (r >= 1 && r <= 32) b->D.krows = (uint32_t)r;
+  }
   if (const char* s = std::getenv("MR_STEP_BUDGET")) b->budget = (uint32_t)std::atoi(s);
   if (b->budget == 0) b->budget = 16384;
   if (mr_batch_reset(b, cfg->seed_base) != 0) {
@@ -454,6 +461,11 @@ static int enqueue_reset(mr_batch* b, uint64_t seed_base) {
   b->resume = false;
   b->D.seed0 = seed_base + b->cfg.cluster_base;
   HIPCHK(hipSetDevice(b->cfg.device));
+  HIPCHK(hipMemsetAsync(b->D.pcnt, 0, CNT__N * sizeof(unsigned long long), b->stream));
+#if MR_GUARD  // a violation belongs to the run it happened in
+  HIPCHK(hipMemsetAsync(b->D.guard, 0, 4 * sizeof(uint32_t), b->stream));
+  b->D.gprobe = std::getenv("MR_GUARD_PROBE") ? 1u : 0u;
+#endif
   HIPCHK(hipMemsetAsync(b->D.stor, 0, (size_t)b->D.C * b->D.apply_cap * sizeof(SE), b->stream));
   if (b->D.led)
     HIPCHK(hipMemsetAsync(b->D.led, 0, (size_t)b->D.C * LED_W * sizeof(uint32_t), b->stream));
@@ -515,6 +527,20 @@ static uint64_t remaining_after(const mr_batch* b) {
   return (uint64_t)b->h_remaining[0] + (b->D.stream && next < b->D.C ? b->D.C - next : 0u);
 }
 
+// MR_GUARD builds: the run fails with the first out-of-range index its launches recorded
+static int guard_check(mr_batch* b) {
+#if MR_GUARD
+  uint32_t g[4];
+  HIPCHK(hipMemcpy(g, b->D.guard, sizeof g, hipMemcpyDeviceToHost));
+  if (g[0])
+    return set_err("MR_GUARD: index " + std::to_string(g[2]) + " out of range " + std::to_string(g[3]) +
+                   " (tag " + std::to_string(g[0]) + ", cluster " + std::to_string(g[1]) + ")");
+#else
+  (void)b;
+#endif
+  return 0;
+}
+
 int mr_batch_reset(mr_batch* b, uint64_t seed_base) {
   if (!b) return set_err("null batch");
   if (b->submitted) return set_err("batch has a submitted step: mr_batch_finish it first");
@@ -558,13 +584,7 @@ int mr_batch_run(mr_batch* b, uint64_t max_events_per_call, mr_run_stats* st) {
     }
   }
   b->D.c0 = 0;
-#if MR_GUARD
-  uint32_t g[4];
-  HIPCHK(hipMemcpy(g, b->D.guard, sizeof g, hipMemcpyDeviceToHost));
-  if (g[0])
-    return set_err("MR_GUARD: index " + std::to_string(g[2]) + " out of range " + std::to_string(g[3]) +
-                   " (tag " + std::to_string(g[0]) + ", cluster " + std::to_string(g[1]) + ")");
-#endif
+  if (guard_check(b) != 0) return -1;
   s.wall_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   // events processed and clusters left: sums over the per-cluster counters (cheap reduce)
   mr_counters c;
@@ -610,6 +630,7 @@ int mr_batch_finish(mr_batch* b, mr_run_stats* st, mr_counters* cnt) {
     s.launches += more.launches;
     s.remaining = more.remaining;
   }
+  if (guard_check(b) != 0) return -1;  // (mr_batch_run above checked its own launches)
   mr_counters c;
   if (mr_batch_counters(b, &c) != 0) return -1;
   s.events = c.events;

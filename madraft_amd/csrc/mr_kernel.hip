@@ -21,6 +21,8 @@
 // observable effect (sends, trace records).
 #include <hip/hip_runtime.h>
 
+#include <atomic>
+
 #include "mr_dev.h"
 
 #ifndef MR_TAPE
@@ -57,6 +59,11 @@ constexpr uint32_t RUN = MR_RUNNING;
 constexpr uint32_t NONE = 0xFFFFFFFFu;
 constexpr uint32_t ELECTION_US = 1000000;  // RAFT_ELECTION_TIMEOUT, tests.rs:18
 
+// entries per batch of independent loads in log walks (A/B round 2: 4 vs 8 +1.7 % figure_8 with
+// 64-lane blocks, profiles/r02_ab_configs.txt r02_s2r; round 3: 2 / 3 / 5 / 6 / 8 -7.0 / -1.7 /
+// -3.3 / -3.3 / -20 %; round 6, the pool: 6 / 8 ±0.3 %, profiles/r06_ab_ac.txt)
+constexpr uint32_t AC = 4;
+
 // per-lane registers of one cluster during a launch
 struct X {
   uint32_t c, now, events, msgs_sent, inflight, code, trace_n, mslot, netmode, t_ctr;
@@ -83,9 +90,11 @@ enum : uint32_t { G_NODE = 1, G_MSG, G_LOG, G_KT_SLOT, G_KT_FIELD, G_KWK, G_KV, 
 #if MR_GUARD
 __device__ __noinline__ uint32_t guard_bad(uint32_t* g, uint32_t tag, uint32_t c, uint32_t i,
                                            uint32_t n) {
-  g[1] = c; g[2] = i; g[3] = n;
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-  g[0] = tag;
+  if (atomicCAS(&g[0], 0u, ~0u) == 0u) {  // the first violation of the run is the one reported
+    g[1] = c; g[2] = i; g[3] = n;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    atomicExch(&g[0], tag);
+  }
   return 0u;
 }
 #define GI(i, n, tag) \
@@ -147,17 +156,45 @@ extern __shared__ uint64_t s_keys_raw[];
 #define s_keys reinterpret_cast<lkey_t*>(s_keys_raw)
 // key rows: one column per lane (step_kernel) or per pool slot (pool_kernel, x.ls)
 constexpr uint32_t KSTR = MR_POOL ? POOL_SLOTS : STEP_BLOCK;
+// the Raft pool's 7-server units (MR_POOL 1, NB 7: up to 64 messages in flight) lay out LDS rows
+// for slots 0..KROWS-1 only, so a pool of 512 clusters fits the CU's LDS: a cluster's slots from
+// D.krows on (KROWS, or fewer: MR_KEY_ROWS, a test knob that exercises the HBM keys) keep their
+// keys in HBM (D.mkey, the key format between launches) — the slot allocator takes the lowest
+// free slot, so those hold a key only while more than krows messages of the cluster are in
+// flight (config 4's peak is 28 per 512 seeds). (The 3- / 5-server pools run M <= 32.)
+constexpr bool KEYS_HBM = MR_POOL == 1 && NB > 5;
+constexpr uint32_t KROWS = KEYS_HBM ? 32u : 0xFFFFFFFFu;
+DI uint32_t key_rows(const Dev& D) { return D.M < KROWS ? D.M : KROWS; }  // LDS layout
+DI uint32_t key_live(const Dev& D) {  // rows in use: slots below hold their key in LDS
+  if constexpr (KEYS_HBM) return D.krows < key_rows(D) ? D.krows : key_rows(D);
+  return key_rows(D);
+}
 #if MR_POOL
-#define LK(s) s_keys[GI(s, D.M, G_LKEY) * KSTR + x.ls]
+#define LK(s) s_keys[GI(s, key_rows(D), G_LKEY) * KSTR + x.ls]
 #else
 #define LK(s) s_keys[GI(s, D.M, G_LKEY) * KSTR + threadIdx.x]
 #endif
+// a message slot's key: its LDS row, or (KEYS_HBM, slots past KROWS) its HBM word
+DI lkey_t lk_get(const Dev& D, const X& x, uint32_t s) {
+  if constexpr (KEYS_HBM)
+    if (s >= key_live(D)) return (lkey_t)MKEY(s);
+  return LK(s);
+}
+DI void lk_set(const Dev& D, const X& x, uint32_t s, lkey_t v) {
+  if constexpr (KEYS_HBM) {
+    if (s >= key_live(D)) {
+      MKEY(s) = v == LKEY_FREE ? ~0ull : (uint64_t)v;
+      return;
+    }
+  }
+  LK(s) = v;
+}
 // per-wave staging after the M key rows: 16 rows of 64 lanes (u32) for each wave of the block —
 // the send loop's next[p] / term at next[p] - 1, the appliers' and the AppendEntries receive's
 // exchange words
 constexpr uint32_t WSTG_ROWS = 2 * MR_MAX_NODES;
 DI uint32_t* wstg(const Dev& D) {
-  return reinterpret_cast<uint32_t*>(s_keys + D.M * KSTR) + (threadIdx.x >> 6) * (WSTG_ROWS * 64u);
+  return reinterpret_cast<uint32_t*>(s_keys + key_rows(D) * KSTR) + (threadIdx.x >> 6) * (WSTG_ROWS * 64u);
 }
 DI uint32_t lane64() { return threadIdx.x & 63u; }
 #define LNX(p) wstg(D)[(p) * 64u + lane64()]
@@ -483,7 +520,7 @@ DI void rescan_min(const Dev& D, X& x) {
       while (occ) {
         const uint32_t s = 64u * w + (uint32_t)__builtin_ctzll(occ);
         occ &= occ - 1ull;
-        const uint32_t k = (uint32_t)LK(s), t = k >> 5;
+        const uint32_t k = (uint32_t)lk_get(D, x, s), t = k >> 5;
         tie = t == bt || (tie && t > bt);
         if (t < bt) { bt = t; bk = k; bs = s; }
       }
@@ -496,7 +533,7 @@ DI void rescan_min(const Dev& D, X& x) {
         while (occ) {
           const uint32_t s = 64u * w + (uint32_t)__builtin_ctzll(occ);
           occ &= occ - 1ull;
-          const uint32_t k = (uint32_t)LK(s);
+          const uint32_t k = (uint32_t)lk_get(D, x, s);
           if ((k >> 5) != bt) continue;
           const uint32_t q = MS32(MF_PAD, s);
           if (q < bq) { bq = q; bk = k; bs = s; }
@@ -621,7 +658,7 @@ DI int net_send(const Dev& D, X& x, uint32_t src, uint32_t& nctr, uint32_t dst, 
     if constexpr (MR_POOL == 2) {
       if (type == M_AE_REQ) x.aem |= 1ull << slot;
     }
-    LK(slot) = (t << 5) | lo;
+    lk_set(D, x, slot, (t << 5) | lo);
     // every message in flight has a smaller seq: a new one is earliest only by time
     if (t < (uint32_t)(x.mmin >> 32)) { x.mmin = ((uint64_t)t << 32) | lo; x.mslot = slot; }
   } else {
@@ -704,10 +741,6 @@ DI void guard_log_write(const Dev& D, X& x, uint32_t L, uint32_t& pexp, uint32_t
 }
 
 // ---------------------------------------------------------------- tester storage
-// entries per batch of independent loads in log walks (A/B round 2: 4 vs 8 +1.7 % figure_8 with
-// 64-lane blocks, profiles/r02_ab_configs.txt r02_s2r; round 3: 2 / 3 / 5 / 6 / 8 -7.0 / -1.7 /
-// -3.3 / -3.3 / -20 %)
-constexpr uint32_t AC = 4;
 constexpr uint32_t AC_APPLY = 5;  // entries per batch in the applier
 DI void storage_snapshot(const Dev& D, X& x, uint32_t i, uint32_t& slen, uint32_t idx) {  // tester.rs:399-402
   if (idx >= D.apply_cap) { fail(D, x, MR_FAIL_SIM_CAPACITY); return; }
@@ -1121,7 +1154,8 @@ DI void ae_load_batch(const Dev& D, const X& x, uint32_t me, const NC& d, uint32
 // kernels −0.2 / −0.8 %, the 3-server 2D kernel +2.2 %; the 15-clerk kvraft kernels +1.5 / +0.3 %
 // (ab21): on where keys are 32-bit (the 7- / 8-server kernels).
 // the 7- / 8-server kernels; not the pool kernels (A/B r05ab1: figure_8_unreliable_2c +2.8 %,
-// its crash variant +3.3 % without it)
+// its crash variant +3.3 % without it; round 6, config 4 on the 7-server pool: +0.9 % with it,
+// profiles/r06_ab_c4.txt — within a box's noise, so off)
 constexpr bool AE_COOP = MR_KEY32 && !MR_POOL;
 constexpr uint32_t AE_COOP_REM = 12;  // entries after the first batch an owner may hand out (LDS rows)
 DI void wave_sync_lds() {
@@ -1288,6 +1322,12 @@ DI void node_event(const Dev& Darg, X& x, bool is_msg, uint32_t tnode, uint32_t 
   }
   const uint2 prange = has_rec ? reinterpret_cast<const uint2*>(NDP(me))[NF_PLO / 2] : make_uint2(0u, 0u);
   if (is_msg) {
+#if MR_GUARD
+    if (D.gprobe && x.c == 0) {  // positive control of the guard (tests/test_guard.py): a read of
+      const uint32_t v = MS32(MF_HDR, D.M);  // the message slot past the table (GI substitutes 0)
+      asm volatile("" ::"v"(v));
+    }
+#endif
     const uint4 m0 = reinterpret_cast<const uint4*>(MSP(slot))[0];
     const uint32_t hdr = m0.x;
     const uint2 m1 = reinterpret_cast<const uint2*>(MSP(slot))[MF_C / 2];
@@ -1296,7 +1336,7 @@ DI void node_event(const Dev& Darg, X& x, bool is_msg, uint32_t tnode, uint32_t 
     type = hdr_type(hdr); src = hdr_src(hdr); inc = hdr_inc(hdr);  // dst = tnode (key)
     k = hdr_k(hdr);
     hdr_bits = hdr;
-    LK(slot) = LKEY_FREE;
+    lk_set(D, x, slot, LKEY_FREE);
     if constexpr (MW == 1) {
       x.free_mask[0] |= 1ull << slot;
       if constexpr (MR_POOL == 2) x.aem &= ~(1ull << slot);
@@ -2189,6 +2229,13 @@ __global__ void __launch_bounds__(256) reduce_kernel(Dev D, unsigned long long* 
   __syncthreads();
   X x;
   x.c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (blockIdx.x == 0 && threadIdx.x < CNT__N) {  // the pool kernels' workgroup sums
+    const unsigned long long v = D.pcnt[threadIdx.x];
+    if (v) {
+      if (threadIdx.x >= CNT_MAX_INFLIGHT) atomicMax(&acc[threadIdx.x], v);
+      else atomicAdd(&acc[threadIdx.x], v);
+    }
+  }
   if (x.c < D.C) {
     for (uint32_t k = 0; k < CNT__N; k++) {
       unsigned long long v = CS(CS_CNT + k);

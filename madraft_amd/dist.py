@@ -18,7 +18,7 @@ SUM_KEYS = ["clusters", "done", "passed", "failed", "events", "ev_msg", "ev_time
             "msgs_sent", "drop_clog", "drop_loss", "drop_overflow", "drop_deliver", "drop_stale",
             "elections", "leaders_elected", "applies", "snapshots", "installs",
             "entries_shipped", "virt_time_us", "kv_ops", "kv_checked", "log_writes",
-            "entries_materialized", "kv_lin_checked"]
+            "entries_materialized", "kv_lin_checked", "coop_entries"]
 MAX_KEYS = ["max_inflight", "max_log", "max_index"]
 COV_KEYS = ["cov_leaders", "cov_events"]
 NO_FAIL = (1 << 63) - 1

@@ -105,9 +105,11 @@ def _pair_worker(rank, world, port, q):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     c = {k: 0 for k in mdist.SUM_KEYS + mdist.MAX_KEYS}
     c.update(first_fail_cluster=[10, 3][rank], first_fail_code=[6, 1][rank], fail_hist={})
+    c.update({k: 3 + rank for k in mdist.SUM_KEYS})  # every count: summed over the ranks
     tot = mdist.allreduce_counters(c)
     if rank == 0:
-        q.put((tot["first_fail_cluster"], tot["first_fail_code"]))
+        q.put((tot["first_fail_cluster"], tot["first_fail_code"],
+               {k: tot[k] for k in mdist.SUM_KEYS}))
     dist.destroy_process_group()
 
 
@@ -122,4 +124,16 @@ def test_first_fail_pair_reduced_together():
     for p in ps:
         p.join(timeout=60)
         assert p.exitcode == 0
-    assert got == (3, 1)
+    assert got[:2] == (3, 1)
+    assert got[2] == {k: 7 for k in mdist.SUM_KEYS}
+
+
+def test_every_count_of_the_abi_is_reduced():
+    """every mr_counters field is summed (SUM_KEYS), taken as a maximum (MAX_KEYS),
+    reduced as the first failure, or a histogram — none reaches the reduced dict as rank 0's
+    local value (coop_entries, ABI 4, was)."""
+    from madraft_amd._abi import MrCounters
+    hist = {"fail_hist", "cov_leaders", "cov_events"}
+    first = {"first_fail_cluster", "first_fail_code"}
+    for name, _ in MrCounters._fields_:
+        assert name in hist or name in first or name in mdist.SUM_KEYS or name in mdist.MAX_KEYS, name

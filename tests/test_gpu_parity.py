@@ -411,3 +411,45 @@ def test_pool_and_step_kernels_agree(hip, monkeypatch, test):
         assert np.array_equal(a, c)
     for k in COUNTER_KEYS:
         assert cp[k] == cs[k], k
+
+
+@pytest.mark.parametrize("test,kw", [("snapshot_install_unreliable_2d", dict(nodes=7)),
+                                     ("snapshot_install_unreliable_crash_2d", dict(nodes=7))])
+@pytest.mark.parametrize("rows", [32, 4])
+def test_seven_server_pool_agrees_with_step_kernel(hip, monkeypatch, test, kw, rows):
+    """Round 6: the 2D bodies at 7 servers (BASELINE config 4) run on the Raft pool, whose LDS
+    holds the keys of message slots 0..31 and HBM those of slots 32..63; same verdicts, times,
+    digests and counters as the step kernel (all 64 keys in LDS). Config 4 peaks at 28 messages in
+    flight per 512 seeds, so the HBM keys are exercised with 4 LDS rows too (MR_KEY_ROWS)."""
+    def run():
+        with hip.Batch(test, 512, **kw) as b:
+            b.run()
+            return b.kernel, b.verdicts(), b.counters()
+    monkeypatch.setenv("MR_KEY_ROWS", str(rows))
+    kp, vp, cp = run()
+    monkeypatch.setenv("MR_POOL", "0")
+    ks, vs, cs = run()
+    assert (kp, ks) == ("pool_kernel", "step_kernel")
+    for a, c in zip(vp, vs):
+        assert np.array_equal(a, c)
+    for k in COUNTER_KEYS:
+        assert cp[k] == cs[k], k
+    if rows < 32:
+        assert cp["max_inflight"] > rows  # slots past the LDS rows were used
+
+
+def test_pool_workgroup_streaming_counters(hip, monkeypatch):
+    """one pool workgroup streams a whole batch (lanes = 512); its 64-bit counter sums
+    (D.pcnt, added by reduce_kernel) equal the step kernel's per-cluster counters."""
+    def run(lanes):
+        with hip.Batch("figure_8_unreliable_2c", 4096, lanes=lanes, iters=40) as b:
+            st = b.run()
+            return b.kernel, st["launches"], b.verdicts(), b.counters()
+    kp, lp, vp, cp = run(512)
+    monkeypatch.setenv("MR_POOL", "0")
+    ks, _, vs, cs = run(0)
+    assert (kp, ks) == ("pool_kernel", "step_kernel")
+    for a, c in zip(vp, vs):
+        assert np.array_equal(a, c)
+    for k in COUNTER_KEYS:
+        assert cp[k] == cs[k], k

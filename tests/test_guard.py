@@ -9,6 +9,12 @@ The GPU test runs the instances that use scratch or faulted before (count_2b, th
 5 and 8 servers — round 3's fault was step_kernel<18, 8> — every kvraft / shard_ctrler test) and
 the headline on the guard library in a child process, and requires no violation and results
 equal to the product library's (verdicts, times and trace digests).
+
+Positive control (verdict r5 weak item 8): with MR_GUARD_PROBE set, the guard library reads one
+message slot past the table (index M) at every message delivery of cluster 0; the run must fail
+with that index, its bound, the message-slot tag and cluster 0 — through mr_batch_run and through
+mr_batch_submit / mr_batch_finish (the bench's path) — and a reset clears the record: the same
+batch then runs clean once the probe is off.
 """
 import json
 import os
@@ -40,6 +46,33 @@ print(json.dumps(out))
 """ % CLUSTERS
 
 
+PROBE_CHILD = r"""
+import os, sys
+from madraft_amd import sim
+out = []
+b = sim.Batch("figure_8_unreliable_2c", 64, iters=60)
+for path in ("run", "submit"):
+    os.environ["MR_GUARD_PROBE"] = "1"
+    try:
+        if path == "run":
+            b.reset(7)
+            b.run()
+        else:
+            b.submit(7)
+            b.finish()
+        out.append(path + ": no error")
+    except sim.SimError as e:
+        out.append(path + ": " + str(e))
+os.environ.pop("MR_GUARD_PROBE")
+b.reset(7)  # the probe is off and the reset clears the previous run's record
+b.run()
+code, _, _ = b.verdicts()
+out.append("clean: %d of %d passed" % (int((code == 0).sum()), len(code)))
+b.close()
+print("\n".join(out))
+"""
+
+
 def test_guard_cases_have_instances():
     """every case names a scenario the guard library builds (an unbuilt one would fail the GPU
     test with 'no instance', not with a guard report)"""
@@ -62,3 +95,22 @@ def test_guard_build_runs_clean(hip):
             rc, rt, rd = b.verdicts()
         assert np.array_equal(rc, code) and np.array_equal(rt, t), (test, kw)
         assert np.array_equal(rd, np.array(dig, np.uint64)), (test, kw)
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(300)
+def test_guard_reports_a_planted_violation(hip):
+    """The guard is not vacuous: a planted out-of-range index is reported exactly (index M = 32
+    message slots of figure_8_unreliable_2c, bound 32, tag G_MSG = 2, cluster 0) on both host
+    paths, and a reset clears it."""
+    assert os.path.exists(build.GUARD_LIB), "the MR_GUARD library is not built (build.build_guard)"
+    env = dict(os.environ, MADRAFT_HIP_LIB=build.GUARD_LIB)
+    env.pop("MR_GUARD_PROBE", None)
+    p = subprocess.run([sys.executable, "-c", PROBE_CHILD], cwd=ROOT, env=env, capture_output=True,
+                       text=True, timeout=280)
+    assert p.returncode == 0, p.stderr[-3000:]
+    run, sub, clean = p.stdout.strip().splitlines()[-3:]
+    want = "MR_GUARD: index 32 out of range 32 (tag 2, cluster 0)"
+    assert run == "run: " + want, run
+    assert sub == "submit: " + want, sub
+    assert clean == "clean: 64 of 64 passed", clean

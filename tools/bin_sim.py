@@ -52,9 +52,13 @@ def per_wave_kernel(seqs, K):
     return max(ends), sum(ends) / len(ends)
 
 
-def binned(seqs, K, move, binc, pick="most", width=64, merge=None):
+def binned(seqs, K, move, binc, pick="most", width=64, merge=None, bank=0, per=1):
     """K waves share the pool; a free wave takes up to `width` ready clusters of one kind.
-    merge: kinds folded together into one bin (e.g. the short node kinds)"""
+    merge: kinds folded together into one bin (e.g. the short node kinds).
+    bank (round 6, verdict r5 item 1): a claim takes at most `per` clusters of each LDS bank
+    class, cluster i's class being i % bank — bank=64: lane b claims a slot with slot % 64 == b;
+    bank=32, per=2: lanes b and b + 32 (the two 32-lane halves of a ds_read_b32 / ds_write_b32,
+    which never conflict with each other) share the slots with slot % 32 == b % 32"""
     merge = merge or {}
     P = len(seqs)
     pos = [0] * P
@@ -88,12 +92,21 @@ def binned(seqs, K, move, binc, pick="most", width=64, merge=None):
                 break
             heapq.heappush(free_at, (release[0][0], w))
             continue
+        def take(lst):
+            if not bank:
+                return lst[:width]
+            cnt, out = {}, []
+            for i in lst:
+                if cnt.get(i % bank, 0) < per and len(out) < width:
+                    cnt[i % bank] = cnt.get(i % bank, 0) + 1
+                    out.append(i)
+            return out
         if pick == "most":
-            k = max(bins, key=lambda k: len(bins[k]))
+            k = max(bins, key=lambda k: len(take(bins[k])))
         else:  # most events per tick of the iteration's cost
-            k = max(bins, key=lambda k: min(width, len(bins[k])) /
-                    (iter_cost([seqs[i][pos[i]] for i in bins[k][:width]]) + move + binc))
-        cl = bins[k][:width]
+            k = max(bins, key=lambda k: len(take(bins[k])) /
+                    (iter_cost([seqs[i][pos[i]] for i in take(bins[k])]) + move + binc))
+        cl = take(bins[k])
         cost = iter_cost([seqs[i][pos[i]] for i in cl]) + move + binc
         for i in cl:
             busy[i] = True
@@ -125,7 +138,9 @@ def main():
                      (f"binned K={K // 2} most", dict(K=K // 2)),
                      (f"binned K={K // 2} rate", dict(K=K // 2, pick="rate")),
                      (f"binned K={K} short", dict(K=K, merge=short)),
-                     (f"binned K={K // 2} short", dict(K=K // 2, merge=short))]:
+                     (f"binned K={K // 2} short", dict(K=K // 2, merge=short)),
+                     (f"binned K={K} bank 64", dict(K=K, bank=64)),
+                     (f"binned K={K} bank 32x2", dict(K=K, bank=32, per=2))]:
         end, it, ev, wt = binned(seqs, move=move, binc=binc, **kw)
         print(f"{name:26s} makespan {end:9.0f} ({base / end:5.2f}x)  iters {it:7d}  "
               f"events/iter {ev / it:5.1f}  ticks/event {wt / ev:6.1f}")

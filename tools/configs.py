@@ -1,8 +1,10 @@
 """BASELINE.json configs 1-5 on one MI355X beside the CPU oracle (dev tool; profiles/r02_configs.txt).
 
-usage: python tools/configs.py [cpu_seconds_per_config]
-Each GPU line: 1 warmup + 2 timed steps of the config's per-GPU batch (kernel ms from HIP
-events, wall seeds/s); each CPU line: the oracle CLI with the same checks, 16 processes, a
+usage: python tools/configs.py [cpu_seconds_per_config] [steps]
+Each GPU line: 1 warmup + `steps` (default 4) timed steps of the config's per-GPU batch, stepped
+as bench.py steps the headline (bench.time_steps: two batches on two streams, step j + 1
+submitted before step j is finished; kernel ms = the launches' HIP-event average, which overlap;
+seeds/s = wall clock); each CPU line: the oracle CLI with the same checks, 16 processes, a
 bounded sample. Config 1 is the reference's single-seed CPU case (GPU column: one cluster).
 """
 import json
@@ -15,10 +17,12 @@ import torch  # noqa: F401  (HIP runtime first)
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))  # repo root
 from madraft_amd import _abi, sim
+from bench import time_steps  # noqa: E402
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 EXE = os.path.join(ROOT, "oracle", "_build", "mr_oracle")
 CPU_S = float(sys.argv[1]) if len(sys.argv) > 1 else 6.0
+STEPS = int(sys.argv[2]) if len(sys.argv) > 2 else 4
 
 CONFIGS = [  # (name, test, clusters per GPU, Batch kwargs, oracle CLI args)
     ("C1 initial_election_2a, 3 nodes, 1 seed", "initial_election_2a", 1, {}, []),
@@ -56,20 +60,18 @@ def cpu_rate(test, args, seconds):
 
 
 for name, test, c, kw, args in CONFIGS:
-    with sim.Batch(test, c, **kw) as b:
-        b.run()
-        ms = ev = 0.0
-        t0 = time.perf_counter()
-        for k in range(2):
-            b.reset(_abi.README_SEED + (k + 1) * c)
-            st = b.run()
-            ms += st["kernel_ms"]
-            ev += st["events"]
-        wall = time.perf_counter() - t0
-        cnt = b.counters()
+    bs = [sim.Batch(test, c, **kw) for _ in range(2 if c > 1 else 1)]
+    wall, acc = time_steps(bs, _abi.README_SEED, c, 1, STEPS, lambda: None)
+    kern = bs[0].kernel
+    for b in bs:
+        b.close()
+    ms = sum(st["kernel_ms"] for st, _ in acc) / STEPS
+    ev = sum(cn["events"] for _, cn in acc)
+    cnt = {k: sum(cn[k] for _, cn in acc) for k in ("passed", "done", "kv_lin_checked")}
     cs, ce, n = cpu_rate(test, args, CPU_S)
-    print(f"{name}: GPU {2 * c / wall:,.0f} seeds/s, {ev / wall / 1e9:.3f} G events/s, "
-          f"{ms / 2:.1f} kernel ms per {c} clusters, pass {cnt['passed']}/{cnt['done']}"
+    print(f"{name}: GPU {STEPS * c / wall:,.0f} seeds/s, {ev / wall / 1e9:.3f} G events/s, "
+          f"{wall * 1000 / STEPS:.1f} ms per step, {ms:.1f} kernel ms per {c} clusters ({kern}), "
+          f"pass {cnt['passed']}/{cnt['done']}"
           + (f", lin-checked Gets {cnt['kv_lin_checked']:,}" if cnt["kv_lin_checked"] else "") + " | "
           f"CPU (oracle, 16 procs, {n} seeds) {cs:,.0f} seeds/s, {ce / 1e6:.1f} M events/s | "
-          f"x{2 * c / wall / cs:.1f}", flush=True)
+          f"x{STEPS * c / wall / cs:.1f}", flush=True)

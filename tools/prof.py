@@ -39,13 +39,13 @@ print(f"total wave-time {tot / 1e8:.4g} s (100 MHz wall clock)")
 for k, name in enumerate(NAMES):
     if v[k] or v[32 + k]:
         print(f"{name:10s} {v[k] / tot * 100:6.2f}%  marks {v[32 + k]:12d}  cyc/mark {v[k] / max(1, v[32 + k]):10.0f}")
-if len(v) >= 89 and any(v[64:89]):  # pool_kernel: per bin (mr_pool.inc PK_*: order by MR_POOL_BINS)
-    for k in range(6):
-        it, cl, cy = v[64 + k], v[70 + k], v[76 + k]
+if len(v) >= 95 and any(v[64:95]):  # pool_kernel: per kind (mr_pool.inc PK_*)
+    for k in range(8):
+        it, cl, cy = v[64 + k], v[72 + k], v[80 + k]
         if it:
             print(f"pool bin {k} iterations {it:10d}  clusters/iter {cl / it:5.1f}  "
                   f"cyc/iter {cy / it:7.0f}  cyc/event {cy / max(1, cl):6.1f}")
-    print(f"pool idle spins {v[82]}  lost claims {v[83]}")
-    if v[88]:  # sums over blocks: crossing times / block lifetimes
+    print(f"pool idle spins {v[88]}  lost claims {v[89]}")
+    if v[94]:  # sums over blocks: crossing times / block lifetimes
         print("pool tail: live < 384 / 256 / 64 / 8 at " +
-              " / ".join(f"{v[84 + q] / v[88]:.3f}" for q in range(4)) + " of the block lifetime")
+              " / ".join(f"{v[90 + q] / v[94]:.3f}" for q in range(4)) + " of the block lifetime")
