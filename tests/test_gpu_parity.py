@@ -167,14 +167,16 @@ def test_small_capacities_fail_identically(hip, oracle):
     ("figure_8_unreliable_2c", dict(nodes=7, log_cap=64, flags=_abi.MR_F_SAFETY)),
     ("figure_8_unreliable_2c", dict(nodes=8, flags=_abi.MR_F_SAFETY | _abi.MR_F_BUG_NO_PREV_CHECK)),
     ("snapshot_install_unreliable_2d", dict(nodes=7))])
-def test_cooperative_append_receive(hip, oracle, test, kw):
+def test_cooperative_append_receive(hip, oracle, monkeypatch, test, kw):
     """The cooperative AppendEntries receive of the 7- / 8-server step kernels (a payload's
-    entries after the first batch spread over the wave; the pool kernel and the 3- / 5-server
+    entries after the first batch spread over the wave; the pool kernels and the 3- / 5-server
     step kernels receive sequentially): full 16-entry
     payloads hitting a tiny log ring (SIM_CAPACITY part-way through the spread entries,
     write-guard materializations), MR_F_SAFETY log matching, a Raft without the prev check
     (whose logs diverge) and snapshot compaction under the spread — all equal to the oracle's
-    sequential walk, and the spread path taken (coop_entries, ABI 4)."""
+    sequential walk, and the spread path taken (coop_entries, ABI 4). The step kernel is forced
+    (MR_POOL=0): since round 6 the 2D bodies at 7 servers run on the Raft pool."""
+    monkeypatch.setenv("MR_POOL", "0")
     code, cnt = compare(hip, oracle, test, 512, traced=3, **kw)
     assert cnt["log_writes"] > 0 and cnt["coop_entries"] > 0
 
