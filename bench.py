@@ -180,6 +180,9 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--clusters", type=int, default=131072, help="clusters (seeds) per GPU")
     ap.add_argument("--test", default="figure_8_unreliable_2c")
+    ap.add_argument("--nodes", type=int, default=0,
+                    help="servers per cluster (0: the test's default; BASELINE config 4 runs the 2D "
+                         "tests at 7)")
     ap.add_argument("--variant", default="figure_8_unreliable_crash",
                     help="second workload timed on the same shard ('' = none)")
     ap.add_argument("--variant-steps", type=int, default=2)
@@ -220,8 +223,9 @@ def main():
 
     total = a.clusters * world
     base, count = mdist.shard(total, world, rank)
+    kw = {"nodes": a.nodes} if a.nodes else {}
     bs = [sim.Batch(a.test, count, _abi.README_SEED, cluster_base=base, device=local,
-                    safety=not a.no_safety) for _ in range(a.pipeline)]
+                    safety=not a.no_safety, **kw) for _ in range(a.pipeline)]
     n = int(bs[0].cfg.n_nodes)
     elapsed, acc = time_steps(bs, _abi.README_SEED, total, a.warmup, a.steps, barrier)
     kernel = bs[0].kernel  # mr_batch_kernel: the kernel the timed launches ran

@@ -1,6 +1,6 @@
 """Section profile of step_kernel (dev tool): needs a library built with -DMR_PROF.
 
-usage: MADRAFT_HIP_LIB=.../libmr_prof.so python tools/prof.py [test] [clusters]
+usage: MADRAFT_HIP_LIB=.../libmr_prof.so python tools/prof.py [test] [clusters] [nodes]
 Runs one batch in a child process (the library prints MRPROF at batch destroy)
 and prints wave cycles per kernel section (mr_kernel.hip P_*).
 """
@@ -18,7 +18,7 @@ if len(sys.argv) > 1 and sys.argv[1] == "--child":
     import torch  # noqa: F401  (HIP runtime first, as in bench.py)
     from madraft_amd.sim import Batch
     test, n = sys.argv[2], int(sys.argv[3])
-    b = Batch(test, n)
+    b = Batch(test, n, **({"nodes": int(sys.argv[4])} if len(sys.argv) > 4 else {}))
     st = b.run()
     code, _, _ = b.verdicts()
     print("run", st, "pass", int((code == 0).sum()), flush=True)
@@ -27,7 +27,8 @@ if len(sys.argv) > 1 and sys.argv[1] == "--child":
 
 test = sys.argv[1] if len(sys.argv) > 1 else "figure_8_unreliable_2c"
 n = sys.argv[2] if len(sys.argv) > 2 else "131072"
-r = subprocess.run([sys.executable, __file__, "--child", test, n], capture_output=True, text=True)
+r = subprocess.run([sys.executable, __file__, "--child", test, n] + sys.argv[3:4], capture_output=True,
+                   text=True)
 print(r.stdout.strip())
 line = [l for l in r.stderr.splitlines() if l.startswith("MRPROF")]
 if r.returncode or not line:
