@@ -32,6 +32,21 @@ def test_bench_single_rank_json():
     assert v["value"] > 0 and v["pass_rate"] > 0.99
 
 
+def test_bench_pipelined_steps_equal_sequential():
+    """bench.py's pipelined steps (--pipeline 2, the default: two batches on two streams, step
+    j + 1 submitted before step j is finished) run the same seeds to the same events and
+    verdicts as one batch at a time (--pipeline 1); with overlapping launches the roofline is
+    taken over the wall clock per step (roofline.time_base)."""
+    args = [sys.executable, "bench.py", "--steps", "3", "--warmup", "1", "--clusters", "4096",
+            "--variant", "", "--million", "0", "--no-cpu-baseline"]
+    two, one = _run(args + ["--pipeline", "2"]), _run(args + ["--pipeline", "1"])
+    for k in ("events_per_seed", "pass_rate"):
+        assert two[k] == one[k], k
+    assert two["roofline"]["alg_bytes_per_launch"] == one["roofline"]["alg_bytes_per_launch"]
+    assert two["roofline"]["time_base"].startswith("wall clock")
+    assert one["roofline"]["time_base"].startswith("HIP-event")
+
+
 def test_bench_two_ranks_one_gpu():
     """`bench.py --gpus 2` starts torch.distributed.run itself; both ranks share
     the card, counters are all-reduced over gloo; cpu_baseline is an N = 1 figure only."""
