@@ -268,6 +268,12 @@ constexpr KvGen kv_gen(uint32_t s) {
     default: return {0, false, false, false, 0, false};
   }
 }
+// the service pool's applier continuation (mr_kernel.hip AP_CAP) is built for the 15-client
+// linearizable body without service snapshots, whose reconnected followers apply long backlogs:
+// same box (profiles/r06_ab_kvap.txt) C5-lin 3A 76.4 K -> 103.8 K seeds/s (+36 %), while built for
+// every service body config 5 (unreliable_3a) lost 21 % and the snapshotting 3B body 2 % (short
+// backlogs: the extra kind and the registers cost more than the balance gains)
+constexpr bool ap_cont(uint32_t s) { return kv_gen(s).lin && kv_gen(s).maxraft == 0; }
 constexpr bool is_ctrl(uint32_t s) { return s == MR_SCN_CTRL_BASIC_4A || s == MR_SCN_CTRL_MULTI_4A; }
 // scenarios served by the clerk / server request path (kvraft + shard_ctrler)
 constexpr bool is_svc(uint32_t s) { return is_kv(s) || is_ctrl(s); }

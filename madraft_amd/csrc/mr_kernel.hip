@@ -76,6 +76,10 @@ struct X {
   uint32_t cnt[CNT__N];  // pool_kernel: the lane's sums over its events (per cluster: POOL_CNT)
   uint32_t ls;  // pool_kernel: the cluster's pool slot (its LDS column)
   uint64_t aem;  // pool_kernel (MR_POOL 2): the message slots that hold AppendEntries requests
+  // pool_kernel (MR_POOL 2): a node event whose applier backlog continues in later iterations
+  // (node_event, AP_CAP): bit 31 pending | node | send mode | reply type | is_msg | kind | inc |
+  // answered pending slots; ra | src << 1; rb; seq
+  uint32_t ap0, ap1, ap2, ap3;
 };
 
 // MR_GUARD (a debug build, build.build_guard; tests/test_guard.py): every computed index into a
@@ -486,7 +490,10 @@ DI void reset_timer(const Dev& D, X& x, uint32_t d, NC& n) {  // raft.rs:260-263
 // the earliest-message rescan four occupied slots per trip, their LDS reads issued together:
 // after the argument laundering (ab20) figure_8_unreliable_2c +1.2 %, crash +0.6 %, C5 +1 %
 // (ab11), the 3-server 2D kernel −1.3 % (ab20): on for 64-bit keys (the 3- / 5-server kernels)
-constexpr bool RESCAN_X4 = !MR_KEY32;
+#ifndef MR_RESCAN_X4_POOL  // (-D override for A/B builds: the four-slot rescan in the pool kernels)
+#define MR_RESCAN_X4_POOL 0
+#endif
+constexpr bool RESCAN_X4 = !MR_KEY32 || (MR_POOL && MR_RESCAN_X4_POOL);
 DI void rescan_min(const Dev& D, X& x) {
   if constexpr (MR_KEY32) {
     uint32_t bt = ~0u, bk = ~0u, bs = 0;
@@ -507,7 +514,7 @@ DI void rescan_min(const Dev& D, X& x) {
           }
           uint32_t k4[4];
 #pragma unroll
-          for (uint32_t q = 0; q < 4; q++) k4[q] = (uint32_t)LK(s4[q]);
+          for (uint32_t q = 0; q < 4; q++) k4[q] = (uint32_t)lk_get(D, x, s4[q]);
 #pragma unroll
           for (uint32_t q = 0; q < 4; q++) {
             if (!v4[q]) continue;
@@ -813,7 +820,8 @@ DI Dev dev_launder(const Dev& D0) {
 }
 
 template <uint32_t S>
-DI void node_apply(const Dev& D, X& x, uint32_t me, NC& d, uint32_t& kvready) {
+DI void node_apply(const Dev& D, X& x, uint32_t me, NC& d, uint32_t& kvready, uint32_t lim = ~0u) {
+  const uint32_t end = d.commit < lim ? d.commit : lim;  // entries applied now: up to end
   constexpr bool KV = is_svc(S);
   const bool snapmode = (x.netmode >> 1) & 1u;
   SE* const sb = D.stor + (size_t)x.c * D.apply_cap;
@@ -830,27 +838,27 @@ DI void node_apply(const Dev& D, X& x, uint32_t me, NC& d, uint32_t& kvready) {
 #pragma unroll
     for (uint32_t j = 0; j < AC_APPLY; j++) {
       const uint32_t i = i0 + j;
-      const bool ok = i <= d.commit && i < D.apply_cap;
+      const bool ok = i <= end && i < D.apply_cap;
       e[j] = ok ? D.log[logi(D, x, me, i)] : LE{};
       const SE s = ok ? sb[i] : SE{};
       m[j] = s.mask;
       sv[j] = s.val;
     }
   };
-  if (d.applied < d.commit) load_batch(d.applied + 1);
-  while (d.applied < d.commit) {
+  if (d.applied < end) load_batch(d.applied + 1);
+  while (d.applied < end) {
     const uint32_t i0 = d.applied + 1;
     LE ce[AC_APPLY];
     uint32_t cm[AC_APPLY];
     uint64_t csv[AC_APPLY];
 #pragma unroll
     for (uint32_t j = 0; j < AC_APPLY; j++) { ce[j] = e[j]; cm[j] = m[j]; csv[j] = sv[j]; }
-    if (i0 + AC_APPLY <= d.commit) load_batch(i0 + AC_APPLY);
+    if (i0 + AC_APPLY <= end) load_batch(i0 + AC_APPLY);
     PROF(P_AP_LOAD);
 #pragma unroll
     for (uint32_t j = 0; j < AC_APPLY; j++) {
       const uint32_t i = i0 + j;
-      if (i > d.commit) break;
+      if (i > end) break;
       d.applied = i;
       if (i >= D.apply_cap) { fail(D, x, MR_FAIL_SIM_CAPACITY); return; }
       CADD(CNT_APPLIES, 1u);
@@ -1299,11 +1307,24 @@ DI bool ae_recv_coop(const Dev& D, X& x, uint32_t me, NC& d, uint32_t src, bool 
 // the whole node event on the laundered argument copy (dev_launder). Same-box A/B, round 4
 // (profiles/r04_ab_round4.txt ab15): figure_8_unreliable_2c 125.6 -> 121.8 ms, its crash variant
 // 67.2 -> 63.6, C5 183 -> 176, C5-lin 561 -> 528 / 690 -> 675; the tester on it too: worse
+// The service pool (MR_POOL 2) caps the applier of an event that does not append at AP_CAP
+// entries: a server catching up on a backlog (a reconnected follower applies hundreds of entries)
+// leaves the rest — and the event's sends, answers, record store and trace record, in their
+// order — to continuation iterations of a kind of their own (x.ap*, mr_pool.inc PK_APPLY), where
+// every lane is such an applier, instead of holding its wave while the other lanes wait. The
+// cluster runs nothing else in between (it is held in that queue), so every effect is the one
+// the uncapped event has.
+// (cap 5 / 10 / 20, C5-lin 3A: 103.8 / 102.2 / 99.5 K seeds/s, profiles/r06_ab_kvap.txt; 5 = one
+// batch of the applier's loads, AC_APPLY)
+constexpr uint32_t AP_CAP = 5;
 template <uint32_t S>
 DI void node_event(const Dev& Darg, X& x, bool is_msg, uint32_t tnode, uint32_t slot,
                    uint32_t seq) {
   const Dev D = dev_launder<S>(Darg);
   constexpr bool KV = is_svc(S);  // kvraft / shard_ctrler request path
+  constexpr bool APC = MR_POOL == 2 && ap_cont(S);
+  const bool apc = APC && (x.ap0 >> 31);  // an applier continuation (see AP_CAP)
+  if (apc) { tnode = x.ap0 & 7u; is_msg = false; }
   uint32_t me = tnode, src = 0, type = 0, inc = 0, k = 0, mterm = 0, ma = 0, mb = 0, mc = 0;
   uint32_t kvready = 0;  // KV: the pending-request slots answered in this event (kv_flush)
   uint32_t hdr_bits = 0;
@@ -1370,7 +1391,12 @@ DI void node_event(const Dev& Darg, X& x, bool is_msg, uint32_t tnode, uint32_t 
 #endif
   uint32_t mode = SEND_NONE, peers = 0, rtype = 0, ra = 0, rb = 0, kind;
   const uint32_t others = ((1u << D.n) - 1u) & ~(1u << me);
-  if (is_msg) {
+  if (apc) {  // the deferred event's tail state
+    mode = (x.ap0 >> 3) & 3u; rtype = (x.ap0 >> 5) & 15u; is_msg = (x.ap0 >> 9) & 1u;
+    kind = (x.ap0 >> 10) & 31u; inc = (x.ap0 >> 15) & 255u; kvready = (x.ap0 >> 23) & 255u;
+    ra = x.ap1 & 1u; src = x.ap1 >> 1; rb = x.ap2; seq = x.ap3;
+    if (mode == SEND_VOTE) peers = others;
+  } else if (is_msg) {
     kind = type;
     if (!bit(x.alive, me) || !bit(x.conn, me) || !bit(x.conn, src) || link_cut(D, x, src, me)) {
       CADD(CNT_DROP_DELIVER, 1u);
@@ -1620,8 +1646,21 @@ DI void node_event(const Dev& Darg, X& x, bool is_msg, uint32_t tnode, uint32_t 
       PROF(P_APPLY);
     }
   } else if (d.applied < d.commit) {
-    node_apply<S>(D, x, me, d, kvready);
+    const bool cap = APC && mode != SEND_APPEND;
+    node_apply<S>(D, x, me, d, kvready, cap ? d.applied + AP_CAP : ~0u);
     if (x.code != RUN) return;
+    if constexpr (APC) {
+      if (cap && d.applied < d.commit) {  // the rest of the backlog, then the tail: later
+        x.ap0 = (1u << 31) | me | (mode << 3) | (rtype << 5) | ((is_msg ? 1u : 0u) << 9) | (kind << 10) |
+                ((inc & 255u) << 15) | (kvready << 23);
+        x.ap1 = (ra & 1u) | (src << 1);
+        x.ap2 = rb;
+        x.ap3 = seq;
+        store_node(D, x, me, d);
+        return;
+      }
+      x.ap0 = 0u;
+    }
     PROF(P_APPLY);
   }
   if (mode == SEND_REPLY) peers = 1u << src;
