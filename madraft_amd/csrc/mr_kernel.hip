@@ -490,10 +490,9 @@ DI void reset_timer(const Dev& D, X& x, uint32_t d, NC& n) {  // raft.rs:260-263
 // the earliest-message rescan four occupied slots per trip, their LDS reads issued together:
 // after the argument laundering (ab20) figure_8_unreliable_2c +1.2 %, crash +0.6 %, C5 +1 %
 // (ab11), the 3-server 2D kernel −1.3 % (ab20): on for 64-bit keys (the 3- / 5-server kernels)
-#ifndef MR_RESCAN_X4_POOL  // (-D override for A/B builds: the four-slot rescan in the pool kernels)
-#define MR_RESCAN_X4_POOL 0
-#endif
-constexpr bool RESCAN_X4 = !MR_KEY32 || (MR_POOL && MR_RESCAN_X4_POOL);
+// (round 6, the pool kernels' 32-bit keys: four slots per trip -0.5 % on config 4, +-0 on the
+// headline, profiles/r06_ab_rx4.txt — off)
+constexpr bool RESCAN_X4 = !MR_KEY32;
 DI void rescan_min(const Dev& D, X& x) {
   if constexpr (MR_KEY32) {
     uint32_t bt = ~0u, bk = ~0u, bs = 0;
