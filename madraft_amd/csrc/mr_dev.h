@@ -273,6 +273,8 @@ constexpr KvGen kv_gen(uint32_t s) {
 // same box (profiles/r06_ab_kvap.txt) C5-lin 3A 76.4 K -> 103.8 K seeds/s (+36 %), while built for
 // every service body config 5 (unreliable_3a) lost 21 % and the snapshotting 3B body 2 % (short
 // backlogs: the extra kind and the registers cost more than the balance gains)
+// (the snapshotting linearizable 3B body with it, cap 5: 89.8 K -> 88.5 K seeds/s, -1.4 %,
+// profiles/r06_ab_kv47.txt)
 constexpr bool ap_cont(uint32_t s) { return kv_gen(s).lin && kv_gen(s).maxraft == 0; }
 constexpr bool is_ctrl(uint32_t s) { return s == MR_SCN_CTRL_BASIC_4A || s == MR_SCN_CTRL_MULTI_4A; }
 // scenarios served by the clerk / server request path (kvraft + shard_ctrler)
