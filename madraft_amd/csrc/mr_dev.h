@@ -276,6 +276,11 @@ constexpr KvGen kv_gen(uint32_t s) {
 // (the snapshotting linearizable 3B body with it, cap 5: 89.8 K -> 88.5 K seeds/s, -1.4 %,
 // profiles/r06_ab_kv47.txt)
 constexpr bool ap_cont(uint32_t s) { return kv_gen(s).lin && kv_gen(s).maxraft == 0; }
+// the KV snapshot copies' chunk (quads whose loads issue together: kv_snapshot, kv_install): 8 for
+// the 15-client linearizable body, 4 for the others. Same box (profiles/r06_ab_kc.txt): the
+// snapshotting linearizable 3B body 89.7 K -> 93.6 K seeds/s with 8 (+4.4 %; 16: -5 %), the 5-client
+// 3B body 238 K -> 220 K (-7.5 %: its kernel spills the larger chunk)
+constexpr uint32_t kv_chunk(uint32_t s) { return kv_gen(s).lin ? 8u : 4u; }
 constexpr bool is_ctrl(uint32_t s) { return s == MR_SCN_CTRL_BASIC_4A || s == MR_SCN_CTRL_MULTI_4A; }
 // scenarios served by the clerk / server request path (kvraft + shard_ctrler)
 constexpr bool is_svc(uint32_t s) { return is_kv(s) || is_ctrl(s); }

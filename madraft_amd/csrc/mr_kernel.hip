@@ -889,7 +889,7 @@ DI void node_apply(const Dev& D, X& x, uint32_t me, NC& d, uint32_t& kvready, ui
           d.snap = i;
           NSV(me) = ce[j].val;
           CADD(CNT_SNAPSHOTS, 1u);
-          kv_snapshot(D, x, me, i);
+          kv_snapshot<kv_chunk(S)>(D, x, me, i);
           if (x.code != RUN) return;
         }
       }
@@ -1581,7 +1581,7 @@ DI void node_event(const Dev& Darg, X& x, bool is_msg, uint32_t tnode, uint32_t 
           storage_snapshot(D, x, me, d.slen, idx);
           if (x.code != RUN) return;
           if constexpr (kv_gen(S).maxraft > 0) {
-            kv_install(D, x, me, idx, kvready);
+            kv_install<kv_chunk(S)>(D, x, me, idx, kvready);
             if (x.code != RUN) return;
           }
           CADD(CNT_INSTALLS, 1u);
