@@ -276,7 +276,7 @@ constexpr KvGen kv_gen(uint32_t s) {
 // (the snapshotting linearizable 3B body with it, cap 5: 89.8 K -> 88.5 K seeds/s, -1.4 %,
 // profiles/r06_ab_kv47.txt)
 constexpr bool ap_cont(uint32_t s) { return kv_gen(s).lin && kv_gen(s).maxraft == 0; }
-// the KV snapshot copies' chunk (quads whose loads issue together: kv_snapshot, kv_install): 8 for
+// the KV snapshot copy's chunk (quads whose loads issue together, kv_snapshot): 8 for
 // the 15-client linearizable body, 4 for the others. Same box (profiles/r06_ab_kc.txt): the
 // snapshotting linearizable 3B body 89.7 K -> 93.6 K seeds/s with 8 (+4.4 %; 16: -5 %), the 5-client
 // 3B body 238 K -> 220 K (-7.5 %: its kernel spills the larger chunk)
